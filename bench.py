@@ -1,0 +1,276 @@
+"""bench.py — training-steps/sec of the MeshGraphNet hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N)
+
+Workload (BASELINE.json configs[1], SURVEY.md §8d Cfg B): CylinderFlow MeshGraphNet, 15 message-passing
+blocks, hidden 128, batch = 8 graphs per GPU (8 jittered copies of the reference's in-tree CylinderFlow
+mesh: N=15,384 nodes, E=88,560 edges per GPU), random-init weights (torch.manual_seed(0)), synthetic
+velocity frames from the same mesh. One step = Simulator train-mode preamble (3 online normalizers,
+one-hot) → EncodeProcessDecode forward → masked L2 loss → backward → [RCCL gradient all-reduce] →
+AdamW(wd 1e-4, β (0.9, 0.95)) → cosine-warmup LR step, exactly the reference training_step
+(lightning_module.py:111-122, 275-292). Inputs are resident in HBM before timing starts.
+
+value = (steps completed by all ranks) / (max-over-ranks wall time of the K timed steps); each rank's
+step is one batch-8 CylinderFlow step, so value/N is the per-GPU step rate (weak scaling).
+Extra JSON fields: roofline (dominant kernel, HIP-event timed over the timed region), cpu_baseline
+(reference-semantics CPU path = oracle, timed on this host's cores, rank 0, N=1), one_step_mse
+(GPU vs reference CPU path on held-out frames with the trained weights), kernels (per-class times).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "graph-physics_amd")]
+
+METRIC = "training-steps/sec + one-step velocity MSE, CylinderFlow MGN 15MP h=128"
+PEAK = {"bf16": 2500.0, "fp32": 157.3}  # TFLOP/s dense (MI355X_MICROARCH.md)
+HBM_PEAK = 8000.0  # GB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="graphs per GPU")
+    ap.add_argument("--mp", type=int, default=15)
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU baseline steps (0: skip)")
+    ap.add_argument("--no-mse", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def flops_per_block(n, e, h):
+    return 12 * h * h * e, 10 * h * h * n  # edge MLP, node MLP (2·Σ in·out per row)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != a.gpus:
+        a.gpus = world
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    import __graft_entry__ as ge
+
+    if rank == 0:
+        ge.build()
+    if world > 1:
+        dist.barrier()
+    ge._paths()
+    from graphphysics import _native as nat
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.distributed import allreduce_gradients, global_masked_mse
+    from graphphysics.training.optim import FusedAdamW
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+    from graphphysics.utils.loss import L2Loss
+    from graphphysics.utils.nodetype import NodeType
+    from graphphysics.utils.scheduler import CosineWarmupScheduler
+
+    nat.load()
+    cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    mesh = meshes.load_cylinder_mesh()
+    b = meshes.cylinder_batch(a.batch, t=0, jitter=0.01, seed=1234 + rank, mesh=mesh)
+    data = Data(x=torch.from_numpy(b["x"]).to(dev), y=torch.from_numpy(b["y"]).to(dev),
+                edge_index=torch.from_numpy(b["edge_index"]).to(dev),
+                edge_attr=torch.from_numpy(b["edge_attr"]).to(dev), pos=torch.from_numpy(b["pos"]).to(dev))
+    N, E = data.x.shape[0], data.edge_index.shape[1]
+    torch.manual_seed(0)
+    model = EncodeProcessDecode(a.mp, 2 + NodeType.SIZE, 3, 2, a.hidden, compute_dtype=cdt)
+    sim = Simulator(2 + NodeType.SIZE, 3, 2, 0, 2, 0, 2, 2, model, dev)
+    if world > 1:
+        sim.set_process_group(dist.group.WORLD)
+    params = list(sim.parameters())
+    opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
+    sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
+    masks = [NodeType.NORMAL, NodeType.OUTFLOW]
+    l2 = L2Loss()
+    node_type = data.x[:, 2]
+
+    def step():
+        net, tdn, _ = sim(data)
+        loss = global_masked_mse(tdn, net, node_type, masks) if world > 1 else \
+            l2(tdn, net, node_type, masks)
+        loss.backward()
+        if world > 1:
+            allreduce_gradients(params)
+        opt.step()
+        sched.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    sim.train()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not a.no_profile:
+        nat.profile_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = nat.profile_collect() if not a.no_profile else {}
+    nat.profile_enable(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    last_loss = float(loss.item())
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    h = a.hidden
+    fe, fn = flops_per_block(N, E, h)
+    kinds = {}
+    for k, (ms, cnt) in prof.items():
+        if cnt:
+            kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2)}
+    # algorithmic work per launch of each kernel class: MFMA FLOPs
+    alg_flops = {"fwd_edge": fe, "fwd_node": fn, "bwd_edge": fe, "bwd_node": fn}
+    roof = None
+    if kinds:
+        dom = max((k for k in kinds if k in alg_flops), key=lambda k: kinds[k]["total_ms"])
+        avg_s = kinds[dom]["total_ms"] / 1000 / kinds[dom]["launches"]
+        ach = alg_flops[dom] / avg_s / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[a.dtype],
+                "unit": "TFLOP/s", "frac": round(ach / PEAK[a.dtype], 4), "traffic": None,
+                "flops_per_launch": alg_flops[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
+        step_flops = 3 * (a.mp * (fe + fn) + 2 * (3 * h + 3 * h * h) * E + 2 * (11 * h + 3 * h * h) * N
+                          + 2 * (3 * h * h + h * 2) * N)
+        roof["step_tflops_per_s"] = round(step_flops * a.steps / dt / 1e12, 2)
+    value = world * a.steps / dt
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+        "data": "synthetic: %d jittered copies of the reference in-tree CylinderFlow mesh per GPU, "
+                "random-init weights (seed 0)" % a.batch,
+        "config": {"workload": "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, h, a.batch),
+                   "nodes_per_gpu": N, "edges_per_gpu": E, "global_batch": a.batch * world,
+                   "parallelism": "dp%d" % world, "graphs_per_sec": round(value * a.batch, 2)},
+        "roofline": roof, "kernels": kinds, "last_loss": last_loss,
+    }
+
+    if not a.no_mse:
+        out["one_step_mse"] = one_step_mse(sim, mesh, dev, a)
+    if world == 1 and a.cpu_steps > 0:
+        out["cpu_baseline"] = cpu_baseline(a, b, mesh)
+        if out["cpu_baseline"]:
+            out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def one_step_mse(sim, mesh, dev, a):
+    """Held-out CylinderFlow frames 3→4 and 4→5 (B=1): eval-mode prediction with the trained weights
+    through libmgn vs through the reference-semantics CPU path (oracle, fp32) with the same weights
+    and normalizer statistics; masked MSE as the reference val_loss (lightning_module.py:168-232)."""
+    from oracle import mgn_oracle as O
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    sim.eval()
+    ref = O.OracleEPD(a.mp, 11, 3, 2, a.hidden)
+    ref.load_state_dict({k: v.detach().float().cpu() for k, v in sim.model.state_dict().items()})
+    osim = O.OracleSimulator(ref, 11, 3, 2)
+    for mine, theirs in ((sim._output_normalizer, osim.out_norm), (sim._node_normalizer, osim.node_norm),
+                         (sim._edge_normalizer, osim.edge_norm)):
+        theirs.acc_sum = mine._acc_sum.detach().cpu().clone()
+        theirs.acc_sum_squared = mine._acc_sum_squared.detach().cpu().clone()
+        theirs.acc_count = mine._acc_count.detach().cpu().clone()
+        theirs.num_acc = mine._num_accumulations.detach().cpu().clone()
+    gm, rm = [], []
+    for t in (3, 4):
+        bb = meshes.cylinder_batch(1, t=t, mesh=mesh)
+        x, y = torch.from_numpy(bb["x"]), torch.from_numpy(bb["y"])
+        ei, ea = torch.from_numpy(bb["edge_index"]), torch.from_numpy(bb["edge_attr"])
+        nt = x[:, 2]
+        keep = ~((nt == 0) | (nt == 5))
+        with torch.no_grad():
+            _, _, pred = sim(Data(x=x.to(dev), y=y.to(dev), edge_index=ei.to(dev), edge_attr=ea.to(dev)))
+            pred = pred.cpu()
+            _, _, pr = osim.forward(x, y, ei, ea, training=False)
+        pred[keep], pr[keep] = y[keep], y[keep]
+        gm.append(O.l2_loss(y, pred, nt).item())
+        rm.append(O.l2_loss(y, pr, nt).item())
+    sim.train()
+    g, r = float(np.mean(gm)), float(np.mean(rm))
+    return {"gpu": g, "reference_cpu": r, "abs_diff": abs(g - r), "target_abs_diff": 1e-5,
+            "frames": "3->4, 4->5 (held out), B=1, weights after the timed steps"}
+
+
+def cpu_baseline(a, b, mesh):
+    """The reference algorithm on the host (oracle = op-for-op restatement of the reference's
+    PyTorch CPU path, pinned to golden vectors), same workload (Cfg B batch 8), fp32, all cores."""
+    from oracle import mgn_oracle as O
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    torch.manual_seed(0)
+    ref = O.OracleEPD(a.mp, 11, 3, 2, a.hidden)
+    osim = O.OracleSimulator(ref, 11, 3, 2)
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
+    x, y = torch.from_numpy(b["x"]), torch.from_numpy(b["y"])
+    ei, ea = torch.from_numpy(b["edge_index"]), torch.from_numpy(b["edge_attr"])
+
+    def step():
+        opt.zero_grad()
+        net, tdn, _ = osim.forward(x, y, ei, ea, True)
+        O.l2_loss(tdn, net, x[:, 2]).backward()
+        opt.step()
+
+    step()  # warm-up
+    ts = []
+    for _ in range(a.cpu_steps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    import platform
+
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": cores, "kind": "port",
+            "sample": "%d timed + 1 warm-up full Cfg B steps (batch 8, N=%d, E=%d), torch %s fp32, median"
+                      % (a.cpu_steps, b["x"].shape[0], b["edge_index"].shape[1], torch.__version__),
+            "cpu": model, "host": platform.node()}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,165 @@
+// Shared device helpers for libmgn (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "mgn.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define MGN_WAVE 64
+#define MGN_THREADS 256
+#define RMS_EPS 1e-8f
+
+// --------------------------------------------------------------------------- MFMA traits
+// D[i][j] += sum_k A[i][k] * B[k][j], 16x16 tile per wave.
+//   f32  (v_mfma_f32_16x16x4_f32):   lane l holds A[l&15][l>>4],          B[l>>4][l&15]
+//   bf16 (v_mfma_f32_16x16x32_bf16): lane l holds A[l&15][8(l>>4)+v],     B[8(l>>4)+v][l&15]
+//   C/D (both): lane l, reg r ->  D[(l>>4)*4 + r][l&15]
+template <class T>
+struct Mf;
+template <>
+struct Mf<float> {
+    static constexpr int VEC = 1, KSTEP = 4;
+    typedef float frag;
+    static __device__ __forceinline__ f4 mma(frag a, frag b, f4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+};
+template <>
+struct Mf<__bf16> {
+    static constexpr int VEC = 8, KSTEP = 32;
+    typedef bf16x8 frag;
+    static __device__ __forceinline__ f4 mma(frag a, frag b, f4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+
+template <class T>
+__device__ __forceinline__ typename Mf<T>::frag ld_frag(const T* p) {
+    return *reinterpret_cast<const typename Mf<T>::frag*>(p);
+}
+
+// --------------------------------------------------------------------------- conversions
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(__bf16 x) { return (float)x; }
+template <class T>
+__device__ __forceinline__ T from_f(float x);
+template <>
+__device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <>
+__device__ __forceinline__ __bf16 from_f<__bf16>(float x) { return (__bf16)x; }
+
+__device__ __forceinline__ float load_any(const void* p, int dtype, int64_t i) {
+    return dtype == MGN_F32 ? reinterpret_cast<const float*>(p)[i]
+                            : (float)reinterpret_cast<const __bf16*>(p)[i];
+}
+
+// 4 consecutive values <-> f4
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ f4 ld4(const __bf16* p) {
+    bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+// 4 consecutive fp32 with only 4-byte alignment guaranteed (parameters in an unpadded flat buffer)
+__device__ __forceinline__ f4 ld4u(const float* p) { return f4{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+__device__ __forceinline__ void st4(__bf16* p, f4 v) {
+    bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+// 16-byte chunks: 4 floats or 8 bf16, returned as floats (up to 8)
+template <class T>
+struct Chunk;
+template <>
+struct Chunk<float> {
+    static constexpr int N = 4;
+    static __device__ __forceinline__ void load(const float* p, float* o) {
+        f4 v = *reinterpret_cast<const f4*>(p);
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+    }
+    static __device__ __forceinline__ void store(float* p, const float* o) {
+        *reinterpret_cast<f4*>(p) = f4{o[0], o[1], o[2], o[3]};
+    }
+};
+template <>
+struct Chunk<__bf16> {
+    static constexpr int N = 8;
+    static __device__ __forceinline__ void load(const __bf16* p, float* o) {
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+    }
+    static __device__ __forceinline__ void store(__bf16* p, const float* o) {
+        bf16x8 v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (__bf16)o[i];
+        *reinterpret_cast<bf16x8*>(p) = v;
+    }
+};
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int rup(int a, int b) { return cdiv(a, b) * b; }
+
+// --------------------------------------------------------------------------- packed weights
+// Forward fragments of W[n][k] (nn.Linear weight [out, in]):
+//   pack[((nt*KS + ks)*64 + lane)*VEC + v] = W[nt*16 + (lane&15)][ks*KSTEP + VEC*(lane>>4) + v]
+// Transposed fragments (A operand of dX = dY·W):
+//   packT[((kt*NS + ns)*64 + lane)*VEC + v] = W[ns*KSTEP + VEC*(lane>>4) + v][kt*16 + (lane&15)]
+// kt runs over round_up(ceil(K/16), 8) tiles so a backward chunk of hidden/16 tiles never reads
+// past the layer. Both use the same per-layer element count.
+__host__ __device__ inline int64_t linear_pack_elems(int n, int k, int dtype) {
+    const int vec = dtype == MGN_BF16 ? 8 : 1, kstep = 4 * vec;
+    int64_t fwd = (int64_t)cdiv(n, 16) * cdiv(k, kstep);
+    int64_t bwd = (int64_t)rup(cdiv(k, 16), 8) * cdiv(n, kstep);
+    return (fwd > bwd ? fwd : bwd) * 64 * vec;
+}
+
+// Layer shapes of build_mlp(in, hidden, out, L)
+__host__ __device__ inline void mlp_layer_shape(const mgn_mlp& m, int l, int* n, int* k) {
+    *k = l == 0 ? m.in_dim : m.hidden;
+    *n = l == m.n_layers - 1 ? m.out_dim : m.hidden;
+}
+
+// --------------------------------------------------------------------------- errors
+void mgn_set_error(const std::string& s);
+#define MGN_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            mgn_set_error(std::string(#expr) + ": " + hipGetErrorString(_e));          \
+            return (int)_e;                                                            \
+        }                                                                              \
+    } while (0)
+#define MGN_REQUIRE(cond, msg)                                                         \
+    do {                                                                               \
+        if (!(cond)) {                                                                 \
+            mgn_set_error(msg);                                                        \
+            return 1000;                                                               \
+        }                                                                              \
+    } while (0)
+#define MGN_LAUNCH_CHECK() MGN_TRY(hipGetLastError())
+
+// --------------------------------------------------------------------------- opt-in profiler
+// Kernel classes timed by mgn_profile_* (HIP events on the launch stream; off by default).
+enum MgnProfKind {
+    PROF_FWD_EDGE = 0, PROF_FWD_NODE, PROF_FWD_DENSE, PROF_BWD_EDGE, PROF_BWD_NODE, PROF_BWD_DENSE,
+    PROF_WGRAD, PROF_WGRAD_REDUCE, PROF_COMBINE, PROF_PACK, PROF_ADAMW, PROF_KINDS
+};
+int mgn_prof_begin(int kind, hipStream_t st);  // returns slot or -1 when disabled
+void mgn_prof_end(int slot, hipStream_t st);
+struct ProfScope {
+    int slot;
+    hipStream_t st;
+    ProfScope(int kind, hipStream_t s) : slot(mgn_prof_begin(kind, s)), st(s) {}
+    ~ProfScope() { mgn_prof_end(slot, st); }
+};

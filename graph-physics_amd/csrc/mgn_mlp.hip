@@ -1,0 +1,1251 @@
+// Fused MLP kernels for the MeshGraphNet processor (gfx950).
+//
+// One workgroup (256 threads = 4 waves) owns a tile of BM rows (edges or nodes) and runs the
+// WHOLE build_mlp chain on it (reference graphphysics/models/layers.py:77-113):
+//   prologue  : stage the layer-0 input rows in LDS. EDGE mode gathers [e ‖ x[dst] ‖ x[src]]
+//               (layers.py:689-690,717 — the `cat` is never materialised in HBM); NODE mode
+//               builds [x ‖ Σ_in-edges m] with the segment sum over target-sorted edges
+//               (PyG propagate aggr="add", layers.py:694-696,744).
+//   layers    : MFMA GEMMs (16x16x32 bf16 or 16x16x4 f32), weights read as pre-packed
+//               1-KiB-per-wave fragments from L2, activations ping-pong in LDS, bias+ReLU
+//               epilogue in registers.
+//   epilogue  : RMSNorm (layers.py:59-74) with a cross-wave row reduction, residual add
+//               (layers.py:698-699), saved activations for the backward.
+// Backward = data-gradient chain per tile (same structure, transposed weight fragments) +
+// weight-gradient GEMMs over row chunks (K = rows) with a fixed-order partial-slab reduction.
+#include <cstring>
+#include <cmath>
+
+#include "mgn_common.h"
+
+namespace {
+
+enum { MODE_DENSE = 0, MODE_EDGE = 1, MODE_NODE = 2 };
+
+template <int NT, int MT>
+struct TileCfg {
+    static constexpr int WN = NT < 4 ? NT : 4;
+    static constexpr int NTW = NT / WN;
+    static constexpr int WM = 4 / WN;
+    static constexpr int MTW = (MT / WM) > 0 ? (MT / WM) : 1;
+};
+
+// One layer: acc[i][j] = D tile (n-tile nt0+i, row-tile mt0+j), A = packed fragments (global),
+// B = LDS rows (row m, contiguous k).
+template <class T, int NT, int MT>
+struct Gemm {
+    using C = TileCfg<NT, MT>;
+    static constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
+    f4 acc[C::NTW][C::MTW];
+    int nt0, mt0;
+    bool active;
+
+    __device__ __forceinline__ void run(const T* __restrict__ wp, int KS, const T* lds, int ldl) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int wn = wave % C::WN, wm = wave / C::WN;
+        nt0 = wn * C::NTW;
+        mt0 = wm * C::MTW;
+        active = mt0 < MT;
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        if (!active) return;
+        const T* bp = lds + (size_t)(mt0 * 16 + (lane & 15)) * ldl + VEC * (lane >> 4);
+        const T* ap = wp + ((size_t)nt0 * KS * 64 + lane) * VEC;
+#pragma unroll 2
+        for (int ks = 0; ks < KS; ++ks) {
+            typename Mf<T>::frag a[C::NTW], b[C::MTW];
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i) a[i] = ld_frag(ap + ((size_t)i * KS + ks) * 64 * VEC);
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j) b[j] = ld_frag(bp + (size_t)j * 16 * ldl + ks * KSTEP);
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(a[i], b[j], acc[i][j]);
+        }
+    }
+    __device__ __forceinline__ int n_of(int i) const { return (nt0 + i) * 16 + ((threadIdx.x & 63) >> 4) * 4; }
+    __device__ __forceinline__ int m_of(int j) const { return (mt0 + j) * 16 + (threadIdx.x & 15); }
+};
+
+struct SrcSeg {
+    const void* p;
+    const int32_t* idx;
+    int64_t ld;
+    int32_t ncols, dtype, coff, pad;
+};
+
+template <class T>
+constexpr int dtype_id() { return sizeof(T) == 4 ? MGN_F32 : MGN_BF16; }
+
+// element (row, col) of a segment as float
+__device__ __forceinline__ float seg_load(const SrcSeg& g, int64_t row, int col) {
+    const int64_t r = g.idx ? (int64_t)g.idx[row] : row;
+    return load_any(g.p, g.dtype, r * g.ld + col);
+}
+
+// Stage rows [row0, row0+BM) of the concatenated segments into LDS In[BM][ldi], zero padding
+// rows >= M and columns [K0, KP).
+template <class T, int BM>
+__device__ void load_tile(T* In, int ldi, int K0, int KP, const SrcSeg* seg, int nseg,
+                          int64_t row0, int64_t M) {
+    constexpr int CH = 16 / sizeof(T);
+    for (int s = 0; s < nseg; ++s) {
+        const SrcSeg g = seg[s];
+        const bool vec = g.dtype == dtype_id<T>() && g.ncols % CH == 0 && g.ld % CH == 0 &&
+                         g.coff % CH == 0;
+        if (vec) {
+            const int cpr = g.ncols / CH;
+            for (int it = threadIdx.x; it < BM * cpr; it += MGN_THREADS) {
+                const int r = it / cpr, c = (it - r * cpr) * CH;
+                const int64_t row = row0 + r;
+                u32x4 v = {0u, 0u, 0u, 0u};
+                if (row < M) {
+                    const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
+                    v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(g.p) + sr * g.ld + c);
+                }
+                *reinterpret_cast<u32x4*>(In + (size_t)r * ldi + g.coff + c) = v;
+            }
+        } else {
+            for (int it = threadIdx.x; it < BM * g.ncols; it += MGN_THREADS) {
+                const int r = it / g.ncols, c = it - r * g.ncols;
+                const int64_t row = row0 + r;
+                const float v = row < M ? seg_load(g, row, c) : 0.f;
+                In[(size_t)r * ldi + g.coff + c] = from_f<T>(v);
+            }
+        }
+    }
+    const int padc = KP - K0;
+    if (padc > 0)
+        for (int it = threadIdx.x; it < BM * padc; it += MGN_THREADS) {
+            const int r = it / padc, c = it - r * padc;
+            In[(size_t)r * ldi + K0 + c] = from_f<T>(0.f);
+        }
+}
+
+// --------------------------------------------------------------------------- forward
+struct FwdArgs {
+    SrcSeg seg[3];
+    int32_t nseg;
+    int32_t L, K0, H, NOUT, has_norm, ldi, ldh;
+    int64_t M;
+    const void* wpack;
+    const float* bias[MGN_MAX_LAYERS];
+    const float* scale;
+    float dinv;
+    // NODE mode aggregation of edge messages m_k = scale_e * (z_k / rden_k)
+    const int32_t* seg_ptr;
+    const void* agg_z;
+    const float* agg_rden;
+    const float* agg_scale;
+    void* agg_save;
+    // outputs
+    void* out;
+    int32_t out_dtype;
+    int64_t out_ld;
+    const void* resid;
+    void* act_save;
+    void* z_save;
+    float* rden_save;
+};
+
+template <class T, int BM, class G>
+__device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float* red, int64_t row0) {
+    using C = typename G::C;
+    const int lane = threadIdx.x & 63;
+    const int wn = (threadIdx.x >> 6) % C::WN;
+    const float* b = a.bias[a.L - 1];
+    if (a.has_norm) {
+        float ss[C::MTW];
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j) {
+            ss[j] = 0.f;
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i) {
+                const f4 bb = ld4u(b + g.n_of(i));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float z = g.acc[i][j][r] + bb[r];
+                    g.acc[i][j][r] = z;
+                    ss[j] += z * z;
+                }
+            }
+            ss[j] += __shfl_xor(ss[j], 16);
+            ss[j] += __shfl_xor(ss[j], 32);
+            if (g.active && lane < 16) red[wn * BM + g.m_of(j)] = ss[j];
+        }
+        __syncthreads();
+        if (!g.active) return;
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j) {
+            const int m = g.m_of(j);
+            float tot = 0.f;
+#pragma unroll
+            for (int w = 0; w < C::WN; ++w) tot += red[w * BM + m];
+            const float q = sqrtf(tot) * a.dinv + RMS_EPS;
+            const int64_t row = row0 + m;
+            if (row >= a.M) continue;
+            if (wn == 0 && lane < 16) a.rden_save[row] = q;
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i) {
+                const int n = g.n_of(i);
+                const f4 s = ld4u(a.scale + n);
+                f4 z = g.acc[i][j], y;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) y[r] = s[r] * (z[r] / q);
+                st4(reinterpret_cast<T*>(a.z_save) + row * a.H + n, z);
+                if (a.resid) {
+                    const f4 x = ld4(reinterpret_cast<const T*>(a.resid) + row * a.H + n);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) y[r] = x[r] + y[r];
+                }
+                if (a.out_dtype == MGN_F32)
+                    st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
+                else
+                    st4(reinterpret_cast<__bf16*>(a.out) + row * a.out_ld + n, y);
+            }
+        }
+    } else {
+        if (!g.active) return;
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j) {
+            const int64_t row = row0 + g.m_of(j);
+            if (row >= a.M) continue;
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i) {
+                const int n = g.n_of(i);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (n + r >= a.NOUT) continue;
+                    float y = g.acc[i][j][r] + b[n + r];
+                    if (a.z_save) reinterpret_cast<T*>(a.z_save)[row * a.H + n + r] = from_f<T>(y);
+                    if (a.rden_save && n + r == 0) a.rden_save[row] = 1.f;
+                    if (a.resid) y = to_f(reinterpret_cast<const T*>(a.resid)[row * a.H + n + r]) + y;
+                    if (a.out_dtype == MGN_F32)
+                        reinterpret_cast<float*>(a.out)[row * a.out_ld + n + r] = y;
+                    else
+                        reinterpret_cast<__bf16*>(a.out)[row * a.out_ld + n + r] = (__bf16)y;
+                }
+            }
+        }
+    }
+}
+
+template <class T, int H, int BM, int MODE>
+__global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
+    constexpr int KSTEP = Mf<T>::KSTEP;
+    constexpr int NTH = H / 16, MT = BM / 16;
+    constexpr int CH = 16 / sizeof(T);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int KP0 = rup(a.K0, KSTEP);
+    T* In = reinterpret_cast<T*>(smem);
+    const int in_elems = BM * a.ldi > BM * a.ldh ? BM * a.ldi : BM * a.ldh;
+    T* P0 = In + in_elems;
+    T* P1 = In;  // In is dead after layer 0
+    float* red = reinterpret_cast<float*>(P0 + BM * a.ldh);
+    const int64_t row0 = (int64_t)blockIdx.x * BM;
+
+    load_tile<T, BM>(In, a.ldi, a.K0, KP0, a.seg, a.nseg, row0, a.M);
+    if (MODE == MODE_NODE) {
+        // aggregation: In[r][H + c] = sum over in-edges k of scale[c] * (z[k][c] / rden[k])
+        constexpr int CPR = H / CH;
+        const T* z = reinterpret_cast<const T*>(a.agg_z);
+        for (int it = threadIdx.x; it < BM * CPR; it += MGN_THREADS) {
+            const int r = it / CPR, c = (it - r * CPR) * CH;
+            const int64_t row = row0 + r;
+            float acc[CH];
+#pragma unroll
+            for (int v = 0; v < CH; ++v) acc[v] = 0.f;
+            if (row < a.M) {
+                float s[CH];
+#pragma unroll
+                for (int v = 0; v < CH; ++v) s[v] = a.agg_scale ? a.agg_scale[c + v] : 1.f;
+                const int kb = a.seg_ptr[row], ke = a.seg_ptr[row + 1];
+                for (int k = kb; k < ke; ++k) {
+                    float zz[CH];
+                    Chunk<T>::load(z + (int64_t)k * H + c, zz);
+                    const float q = a.agg_rden[k];
+#pragma unroll
+                    for (int v = 0; v < CH; ++v) acc[v] += s[v] * (zz[v] / q);
+                }
+                Chunk<T>::store(reinterpret_cast<T*>(a.agg_save) + row * H + c, acc);
+            }
+            Chunk<T>::store(In + (size_t)r * a.ldi + H + c, acc);
+        }
+    }
+    __syncthreads();
+
+    const T* wp = reinterpret_cast<const T*>(a.wpack);
+    const T* cur = In;
+    int ldc = a.ldi, KS = KP0 / KSTEP, K = a.K0;
+    for (int l = 0; l < a.L - 1; ++l) {
+        Gemm<T, NTH, MT> g;
+        g.run(wp, KS, cur, ldc);
+        T* nxt = (l & 1) ? P1 : P0;
+        if (g.active) {
+            const float* b = a.bias[l];
+#pragma unroll
+            for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i) {
+                const int n = g.n_of(i);
+                const f4 bb = ld4u(b + n);
+#pragma unroll
+                for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
+                    const int m = g.m_of(j);
+                    f4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(g.acc[i][j][r] + bb[r], 0.f);
+                    st4(nxt + (size_t)m * a.ldh + n, v);
+                    const int64_t row = row0 + m;
+                    if (row < a.M) st4(reinterpret_cast<T*>(a.act_save) + ((int64_t)l * a.M + row) * H + n, v);
+                }
+            }
+        }
+        if (H % KSTEP != 0) {
+            constexpr int padc = (H + KSTEP - 1) / KSTEP * KSTEP - H;
+            for (int it = threadIdx.x; it < BM * padc; it += MGN_THREADS)
+                nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
+        }
+        __syncthreads();
+        wp += linear_pack_elems(H, K, dtype_id<T>());
+        cur = nxt;
+        ldc = a.ldh;
+        KS = cdiv(H, KSTEP);
+        K = H;
+    }
+    if (a.NOUT == H) {
+        Gemm<T, NTH, MT> g;
+        g.run(wp, KS, cur, ldc);
+        fwd_last_epilogue<T, BM>(g, a, red, row0);
+    } else {
+        Gemm<T, 1, MT> g;
+        g.run(wp, KS, cur, ldc);
+        fwd_last_epilogue<T, BM>(g, a, red, row0);
+    }
+}
+
+// --------------------------------------------------------------------------- backward (data)
+struct BwdArgs {
+    int64_t M;
+    int32_t L, K0, H, NOUT, has_norm, ldh, mode;
+    float dinv;
+    const void* wtpack;
+    const float* scale;
+    const void* act_save;
+    const void* z_save;
+    const float* rden_save;
+    const void* dout;
+    int32_t dout_dtype;
+    int64_t dout_ld;
+    const void* gath;       // EDGE: d_aggr [N][H] (T), added at gath_idx[row]
+    const int32_t* gath_idx;
+    void* dz_save;          // [L][M][H] (T)
+    float* dscale_part;     // [gridDim.x][NOUT]
+    void* din;              // DENSE: [M][din_ld] (din_dtype), optional
+    int32_t din_dtype;
+    int64_t din_ld;
+    void* o1;               // EDGE: de_in [M][H]; NODE: dx_part [M][H]  (T)
+    void* o2;               // EDGE: dxij [M][2H]; NODE: d_aggr [M][H]   (T)
+};
+
+template <class T, int H, int BM, int MODE>
+__global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
+    constexpr int KSTEP = Mf<T>::KSTEP, VEC = Mf<T>::VEC;
+    constexpr int NTH = H / 16, MT = BM / 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* D0 = reinterpret_cast<T*>(smem);
+    T* D1 = D0 + BM * a.ldh;
+    float* red = reinterpret_cast<float*>(D1 + BM * a.ldh);  // [256][4]
+    const int64_t row0 = (int64_t)blockIdx.x * BM;
+    const int tid = threadIdx.x;
+    const int NO = a.NOUT;
+    const int KPN = rup(NO, KSTEP);
+
+    // ---- dY -> dZ_last (RMSNorm backward), chunks of 4 columns; CPR lanes per row
+    {
+        const int CPR = cdiv(NO, 4);  // <= 32, divides 256 for NOUT in {H} or <= 16 rounded
+        const int RPP = MGN_THREADS / CPR;  // rows per pass
+        const int cc = (tid % CPR) * 4, rr = tid / CPR;
+        f4 dsc = {0.f, 0.f, 0.f, 0.f};
+        f4 s = {1.f, 1.f, 1.f, 1.f};
+        if (a.has_norm) s = ld4u(a.scale + cc);
+        for (int r = rr; r < BM; r += RPP) {
+            const int64_t row = row0 + r;
+            f4 dy = {0.f, 0.f, 0.f, 0.f};
+            const bool valid = row < a.M && rr < RPP;
+            if (valid) {
+                if (NO % 4 == 0) {
+                    dy = a.dout_dtype == MGN_F32
+                             ? ld4(reinterpret_cast<const float*>(a.dout) + row * a.dout_ld + cc)
+                             : ld4(reinterpret_cast<const __bf16*>(a.dout) + row * a.dout_ld + cc);
+                } else {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        dy[v] = cc + v < NO ? load_any(a.dout, a.dout_dtype, row * a.dout_ld + cc + v) : 0.f;
+                }
+                if (MODE == MODE_EDGE) {
+                    const f4 g = ld4(reinterpret_cast<const T*>(a.gath) + (int64_t)a.gath_idx[row] * H + cc);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) dy[v] += g[v];
+                }
+            }
+            f4 dz = dy;
+            if (a.has_norm) {
+                f4 z = {0.f, 0.f, 0.f, 0.f};
+                float q = 1.f;
+                if (valid) {
+                    z = ld4(reinterpret_cast<const T*>(a.z_save) + row * H + cc);
+                    q = a.rden_save[row];
+                }
+                float dot = 0.f;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) dot += s[v] * dy[v] * z[v];
+                for (int o = 1; o < CPR; o <<= 1) dot += __shfl_xor(dot, o);
+                const float rms = q - RMS_EPS;
+                const float coef = rms > 0.f ? dot / (q * q * rms) * (a.dinv * a.dinv) : 0.f;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    dz[v] = s[v] * dy[v] / q - z[v] * coef;
+                    dsc[v] += dy[v] * (z[v] / q);
+                }
+            }
+            if (r < BM) {
+                st4(D0 + (size_t)r * a.ldh + cc, dz);
+                if (valid) st4(reinterpret_cast<T*>(a.dz_save) + ((int64_t)(a.L - 1) * a.M + row) * H + cc, dz);
+            }
+        }
+        // zero pad columns [NO4, KPN) of D0
+        const int NO4 = CPR * 4;
+        const int padc = KPN - NO4;
+        if (padc > 0)
+            for (int it = tid; it < BM * padc; it += MGN_THREADS) {
+                const int r = it / padc, c = it - r * padc;
+                D0[(size_t)r * a.ldh + NO4 + c] = from_f<T>(0.f);
+            }
+        if (a.has_norm) {
+            *reinterpret_cast<f4*>(red + tid * 4) = dsc;
+            __syncthreads();
+            if (tid < CPR) {
+                f4 t = {0.f, 0.f, 0.f, 0.f};
+                for (int q2 = 0; q2 < RPP; ++q2) {
+                    const f4 u = *reinterpret_cast<const f4*>(red + (q2 * CPR + tid) * 4);
+                    t += u;
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (tid * 4 + v < NO) a.dscale_part[(int64_t)blockIdx.x * NO + tid * 4 + v] = t[v];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- layers L-1 .. 1 : dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]
+    const T* wt = reinterpret_cast<const T*>(a.wtpack);
+    int64_t off[MGN_MAX_LAYERS];
+    {
+        int64_t o = 0;
+        for (int l = 0; l < a.L; ++l) {
+            off[l] = o;
+            const int n = l == a.L - 1 ? NO : H, k = l == 0 ? a.K0 : H;
+            o += linear_pack_elems(n, k, dtype_id<T>());
+        }
+    }
+    T* cur = D0;
+    T* nxt = D1;
+    for (int l = a.L - 1; l >= 1; --l) {
+        const int Nl = l == a.L - 1 ? NO : H;
+        Gemm<T, NTH, MT> g;
+        g.run(wt + off[l], cdiv(Nl, KSTEP), cur, a.ldh);
+        if (g.active) {
+#pragma unroll
+            for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i) {
+                const int k = g.n_of(i);
+#pragma unroll
+                for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
+                    const int m = g.m_of(j);
+                    const int64_t row = row0 + m;
+                    f4 v = g.acc[i][j];
+                    if (row < a.M) {
+                        const f4 act = ld4(reinterpret_cast<const T*>(a.act_save) + ((int64_t)(l - 1) * a.M + row) * H + k);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = act[r] > 0.f ? v[r] : 0.f;
+                        st4(reinterpret_cast<T*>(a.dz_save) + ((int64_t)(l - 1) * a.M + row) * H + k, v);
+                    } else {
+                        v = f4{0.f, 0.f, 0.f, 0.f};
+                    }
+                    st4(nxt + (size_t)m * a.ldh + k, v);
+                }
+            }
+        }
+        if (H % KSTEP != 0) {
+            constexpr int padc = (H + KSTEP - 1) / KSTEP * KSTEP - H;
+            for (int it = tid; it < BM * padc; it += MGN_THREADS)
+                nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
+        }
+        __syncthreads();
+        T* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+
+    // ---- layer 0 : dA0 = dZ_0 · W_0, K0 columns in chunks of H
+    if (MODE == MODE_DENSE && a.din == nullptr) return;
+    const int KS0 = cdiv(a.L == 1 ? NO : H, KSTEP);
+    const int nchunk = cdiv(cdiv(a.K0, 16), NTH);
+    for (int c = 0; c < nchunk; ++c) {
+        Gemm<T, NTH, MT> g;
+        g.run(wt + off[0] + (int64_t)c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+        if (!g.active) continue;
+#pragma unroll
+        for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i) {
+            const int n = g.n_of(i);  // column within the chunk
+#pragma unroll
+            for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
+                const int64_t row = row0 + g.m_of(j);
+                if (row >= a.M) continue;
+                const f4 v = g.acc[i][j];
+                if (MODE == MODE_DENSE) {
+                    const int k = c * H + n;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (k + r < a.K0) {
+                            if (a.din_dtype == MGN_F32)
+                                reinterpret_cast<float*>(a.din)[row * a.din_ld + k + r] = v[r];
+                            else
+                                reinterpret_cast<__bf16*>(a.din)[row * a.din_ld + k + r] = (__bf16)v[r];
+                        }
+                } else if (c == 0) {
+                    const f4 d = ld4(reinterpret_cast<const T*>(a.dout) + row * a.dout_ld + n);
+                    st4(reinterpret_cast<T*>(a.o1) + row * H + n, d + v);
+                } else if (MODE == MODE_EDGE) {
+                    st4(reinterpret_cast<T*>(a.o2) + row * (2 * H) + (c - 1) * H + n, v);
+                } else {
+                    st4(reinterpret_cast<T*>(a.o2) + row * H + n, v);
+                }
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------- weight gradients
+struct WgJob {
+    int32_t layer, kb, n, k;
+    int64_t w_off, b_off;  // offsets in the flat grad vector; b_off < 0: no bias for this job
+};
+struct WgArgs {
+    int64_t M;
+    int32_t rows_per_chunk, H, njobs, nseg;
+    const void* dz_save;
+    const void* act_save;
+    SrcSeg seg[3];
+    WgJob job[12];
+    float* part;
+    int64_t G;
+};
+
+// Transposed staging of SR rows: dst[col][m] for col in [0, H), m in [0, SR).
+template <class T, int H, int SR>
+__device__ void stage_T_from(T* dst, int ldt, const T* src, int64_t src_ld, int ncols, int64_t r0,
+                             int64_t r1) {
+    constexpr int RG = 16 / sizeof(T);  // rows per 16-byte LDS write
+    constexpr int ITEMS = (H / 2) * (SR / RG);
+    for (int it = threadIdx.x; it < ITEMS; it += MGN_THREADS) {
+        const int cp = it % (H / 2), rg = it / (H / 2);
+        const int c = cp * 2, m0 = rg * RG;
+        float v0[RG], v1[RG];
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            const int64_t row = r0 + m0 + q;
+            v0[q] = 0.f;
+            v1[q] = 0.f;
+            if (row < r1 && c < ncols) {
+                const T* p = src + row * src_ld + c;
+                v0[q] = to_f(p[0]);
+                if (c + 1 < ncols) v1[q] = to_f(p[1]);
+            }
+        }
+        Chunk<T>::store(dst + (size_t)c * ldt + m0, v0);
+        Chunk<T>::store(dst + (size_t)(c + 1) * ldt + m0, v1);
+    }
+}
+
+template <class T, int H, int SR>
+__device__ void stage_T_segs(T* dst, int ldt, const SrcSeg* seg, int nseg, int kcol0, int K,
+                             int64_t r0, int64_t r1) {
+    constexpr int RG = 16 / sizeof(T);
+    constexpr int ITEMS = (H / 2) * (SR / RG);
+    for (int it = threadIdx.x; it < ITEMS; it += MGN_THREADS) {
+        const int cp = it % (H / 2), rg = it / (H / 2);
+        const int c = cp * 2, m0 = rg * RG;
+        float v0[RG], v1[RG];
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            v0[q] = 0.f;
+            v1[q] = 0.f;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kc = kcol0 + c + h;
+            if (kc >= K) continue;
+            int s = 0;
+            while (s + 1 < nseg && kc >= seg[s + 1].coff) ++s;
+            const SrcSeg& g = seg[s];
+            const int cl = kc - g.coff;
+#pragma unroll
+            for (int q = 0; q < RG; ++q) {
+                const int64_t row = r0 + m0 + q;
+                if (row < r1) {
+                    const float v = seg_load(g, row, cl);
+                    if (h == 0) v0[q] = v; else v1[q] = v;
+                }
+            }
+        }
+        Chunk<T>::store(dst + (size_t)c * ldt + m0, v0);
+        Chunk<T>::store(dst + (size_t)(c + 1) * ldt + m0, v1);
+    }
+}
+
+template <class T, int H>
+__global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
+    constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
+    constexpr int SR = 64;
+    constexpr int LDT = SR + 16 / sizeof(T);
+    constexpr int NT = H / 16;
+    using C = TileCfg<NT, NT>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* ZT = reinterpret_cast<T*>(smem);
+    T* AT = ZT + H * LDT;
+    const WgJob job = a.job[blockIdx.y];
+    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
+    const int64_t r_end = r_begin + a.rows_per_chunk < a.M ? r_begin + a.rows_per_chunk : a.M;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wn = wave % C::WN, wm = wave / C::WN;
+    const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
+    const bool active = mt0 < NT;
+    f4 acc[C::NTW][C::MTW];
+#pragma unroll
+    for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float bacc = 0.f;
+    const T* dz = reinterpret_cast<const T*>(a.dz_save) + (int64_t)job.layer * a.M * H;
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += SR) {
+        stage_T_from<T, H, SR>(ZT, LDT, dz, H, job.n, r0, r_end);
+        if (job.layer == 0)
+            stage_T_segs<T, H, SR>(AT, LDT, a.seg, a.nseg, job.kb * H, job.k, r0, r_end);
+        else
+            stage_T_from<T, H, SR>(AT, LDT,
+                                   reinterpret_cast<const T*>(a.act_save) + (int64_t)(job.layer - 1) * a.M * H,
+                                   H, H, r0, r_end);
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int ks = 0; ks < SR / KSTEP; ++ks) {
+                typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+                    fa[i] = ld_frag(ZT + (size_t)((nt0 + i) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+#pragma unroll
+                for (int j = 0; j < C::MTW; ++j)
+                    fb[j] = ld_frag(AT + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
+            }
+        }
+        if (job.b_off >= 0 && threadIdx.x < H) {
+            const T* zr = ZT + (size_t)threadIdx.x * LDT;
+            for (int m = 0; m < SR; ++m) bacc += to_f(zr[m]);
+        }
+        __syncthreads();
+    }
+    float* part = a.part + (int64_t)blockIdx.x * a.G;
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j) {
+                const int kc = job.kb * H + (mt0 + j) * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = (nt0 + i) * 16 + (lane >> 4) * 4 + r;
+                    if (n < job.n && kc < job.k) part[job.w_off + (int64_t)n * job.k + kc] = acc[i][j][r];
+                }
+            }
+    }
+    if (job.b_off >= 0 && threadIdx.x < job.n) part[job.b_off + threadIdx.x] = bacc;
+}
+
+// grads[g] = Σ_c part[c][g] (g < G);  grads[G + s] = Σ_t dscale_part[t][s] (s < NS)
+__global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(const float* __restrict__ part, int nchunks,
+                                                                   int64_t G, const float* __restrict__ dsp,
+                                                                   int ntiles, int NS, float* __restrict__ grads) {
+    const int64_t g = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x;
+    if (g < G) {
+        float s = 0.f;
+        for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * G + g];
+        grads[g] = s;
+    } else if (g < G + NS) {
+        const int sidx = (int)(g - G);
+        float s = 0.f;
+        for (int t = 0; t < ntiles; ++t) s += dsp[(int64_t)t * NS + sidx];
+        grads[g] = s;
+    }
+}
+
+// --------------------------------------------------------------------------- weight packing
+template <class T>
+__global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* jobs) {
+    const mgn_pack_job j = jobs[blockIdx.y];
+    if (j.dtype != dtype_id<T>()) return;
+    constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
+    const int n = j.n, k = j.k;
+    const int KS = cdiv(k, KSTEP), NTp = cdiv(n, 16);
+    const int NS = cdiv(n, KSTEP), KTp = rup(cdiv(k, 16), 8);
+    const int64_t tot = linear_pack_elems(n, k, dtype_id<T>());
+    T* dst = reinterpret_cast<T*>(j.dst);
+    T* dstT = reinterpret_cast<T*>(j.dstT);
+    for (int64_t e = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x; e < tot; e += (int64_t)gridDim.x * MGN_THREADS) {
+        const int v = (int)(e % VEC);
+        const int64_t fl = e / VEC;
+        const int lane = (int)(fl % 64);
+        const int64_t tile = fl / 64;
+        {  // forward: tile = nt*KS + ks
+            float w = 0.f;
+            if (tile < (int64_t)NTp * KS) {
+                const int nt = (int)(tile / KS), ks = (int)(tile % KS);
+                const int nn = nt * 16 + (lane & 15), kk = ks * KSTEP + VEC * (lane >> 4) + v;
+                if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
+            }
+            dst[e] = from_f<T>(w);
+        }
+        {  // transposed: tile = kt*NS + ns
+            float w = 0.f;
+            if (tile < (int64_t)KTp * NS) {
+                const int kt = (int)(tile / NS), ns = (int)(tile % NS);
+                const int kk = kt * 16 + (lane & 15), nn = ns * KSTEP + VEC * (lane >> 4) + v;
+                if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
+            }
+            dstT[e] = from_f<T>(w);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------- host side
+template <class T>
+constexpr int bm_of() { return sizeof(T) == 4 ? 32 : 64; }
+
+int set_lds(const void* fn, size_t bytes) {
+    if (bytes > 65536)
+        MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    return 0;
+}
+
+template <class T>
+int pad_ld(int cols) {
+    return cols + (int)(16 / sizeof(T));
+}
+
+int check_mlp(const mgn_mlp* m) {
+    MGN_REQUIRE(m != nullptr, "mlp descriptor is NULL");
+    MGN_REQUIRE(m->n_layers >= 2 && m->n_layers <= MGN_MAX_LAYERS,
+                "The MLP must have at least 2 layers (input and output) and at most 8");
+    MGN_REQUIRE(m->hidden == 16 || m->hidden == 32 || m->hidden == 64 || m->hidden == 128,
+                "hidden size must be one of 16, 32, 64, 128");
+    MGN_REQUIRE(m->in_dim >= 1, "in_dim must be >= 1");
+    MGN_REQUIRE(m->out_dim == m->hidden || (m->out_dim >= 1 && m->out_dim <= 16),
+                "out_dim must equal hidden or be in [1, 16]");
+    MGN_REQUIRE(!m->has_norm || m->out_dim == m->hidden, "RMSNorm requires out_dim == hidden");
+    MGN_REQUIRE(m->dtype == MGN_F32 || m->dtype == MGN_BF16, "dtype must be MGN_F32 or MGN_BF16");
+    MGN_REQUIRE(m->wpack && m->wtpack, "packed weights missing");
+    for (int l = 0; l < m->n_layers; ++l) MGN_REQUIRE(m->bias[l], "bias pointer missing");
+    MGN_REQUIRE(!m->has_norm || m->scale, "RMSNorm scale pointer missing");
+    return 0;
+}
+
+struct MlpIn {
+    SrcSeg seg[3];
+    int nseg;
+};
+
+template <class T, int H, int MODE>
+int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_dtype, int64_t out_ld,
+               const void* resid, mgn_mlp_saved* sv, const mgn_topology* topo, const mgn_mlp* agg_mlp,
+               const mgn_mlp_saved* agg_sv, void* agg_save, hipStream_t st) {
+    constexpr int BM = bm_of<T>();
+    FwdArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int s = 0; s < in.nseg; ++s) a.seg[s] = in.seg[s];
+    a.nseg = in.nseg;
+    a.L = m->n_layers;
+    a.K0 = m->in_dim;
+    a.H = H;
+    a.NOUT = m->out_dim;
+    a.has_norm = m->has_norm;
+    a.ldi = pad_ld<T>(rup(m->in_dim, Mf<T>::KSTEP));
+    a.ldh = pad_ld<T>(rup(H, Mf<T>::KSTEP));
+    a.M = M;
+    a.wpack = m->wpack;
+    for (int l = 0; l < m->n_layers; ++l) a.bias[l] = m->bias[l];
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)m->out_dim));
+    if (MODE == MODE_NODE) {
+        a.seg_ptr = topo->col_ptr;
+        a.agg_z = agg_sv->z;
+        a.agg_rden = agg_sv->rden;
+        a.agg_scale = agg_mlp->scale;
+        a.agg_save = agg_save;
+    }
+    a.out = out;
+    a.out_dtype = out_dtype;
+    a.out_ld = out_ld;
+    a.resid = resid;
+    a.act_save = sv->act;
+    a.z_save = sv->z;
+    a.rden_save = sv->rden;
+    const size_t in_elems = (size_t)BM * (a.ldi > a.ldh ? a.ldi : a.ldh);
+    const size_t lds = (in_elems + (size_t)BM * a.ldh) * sizeof(T) + 4 * BM * sizeof(float);
+    auto fn = mlp_fwd_kernel<T, H, BM, MODE>;
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    const int grid = (int)cdiv64(M, BM);
+    if (grid == 0) return 0;
+    ProfScope ps(MODE == MODE_EDGE ? PROF_FWD_EDGE : MODE == MODE_NODE ? PROF_FWD_NODE : PROF_FWD_DENSE, st);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+struct BwdOut {
+    int mode;
+    const void* gath;
+    const int32_t* gath_idx;
+    void* din;
+    int din_dtype;
+    int64_t din_ld;
+    void* o1;
+    void* o2;
+};
+
+template <class T, int H, int MODE>
+int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, int dout_dtype,
+               int64_t dout_ld, const BwdOut& o, void* dz_save, float* dscale_part, hipStream_t st) {
+    constexpr int BM = bm_of<T>();
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.M = M;
+    a.L = m->n_layers;
+    a.K0 = m->in_dim;
+    a.H = H;
+    a.NOUT = m->out_dim;
+    a.has_norm = m->has_norm;
+    a.ldh = pad_ld<T>(rup(H, Mf<T>::KSTEP));
+    a.mode = MODE;
+    a.dinv = (float)(1.0 / sqrt((double)m->out_dim));
+    a.wtpack = m->wtpack;
+    a.scale = m->scale;
+    a.act_save = sv->act;
+    a.z_save = sv->z;
+    a.rden_save = sv->rden;
+    a.dout = dout;
+    a.dout_dtype = dout_dtype;
+    a.dout_ld = dout_ld;
+    a.gath = o.gath;
+    a.gath_idx = o.gath_idx;
+    a.dz_save = dz_save;
+    a.dscale_part = dscale_part;
+    a.din = o.din;
+    a.din_dtype = o.din_dtype;
+    a.din_ld = o.din_ld;
+    a.o1 = o.o1;
+    a.o2 = o.o2;
+    const size_t lds = 2 * (size_t)BM * a.ldh * sizeof(T) + MGN_THREADS * 4 * sizeof(float);
+    auto fn = mlp_bwd_kernel<T, H, BM, MODE>;
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    const int grid = (int)cdiv64(M, BM);
+    if (grid == 0) return 0;
+    ProfScope ps(MODE == MODE_EDGE ? PROF_BWD_EDGE : MODE == MODE_NODE ? PROF_BWD_NODE : PROF_BWD_DENSE, st);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+// flat grad vector size (excluding RMSNorm scale)
+int64_t grad_G(const mgn_mlp* m) {
+    int64_t g = 0;
+    for (int l = 0; l < m->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*m, l, &n, &k);
+        g += (int64_t)n * k + n;
+    }
+    return g;
+}
+
+int wgrad_rows_per_chunk(const mgn_mlp* m, int64_t M) {
+    const int H = m->hidden;
+    int jobs = cdiv(m->in_dim, H) + (m->n_layers - 1);
+    int64_t target = 1024 / jobs;
+    if (target < 1) target = 1;
+    int64_t r = cdiv64(M, target);
+    r = cdiv64(r, 64) * 64;
+    if (r < 256) r = 256;
+    return (int)r;
+}
+
+template <class T, int H>
+int launch_wgrad(const mgn_mlp* m, int64_t M, const MlpIn& in, const void* act_save, const void* dz_save,
+                 const float* dscale_part, int ntiles, float* part, float* grads, hipStream_t st) {
+    WgArgs a;
+    memset(&a, 0, sizeof(a));
+    a.M = M;
+    a.H = H;
+    a.rows_per_chunk = wgrad_rows_per_chunk(m, M);
+    a.dz_save = dz_save;
+    a.act_save = act_save;
+    for (int s = 0; s < in.nseg; ++s) a.seg[s] = in.seg[s];
+    a.nseg = in.nseg;
+    a.part = part;
+    a.G = grad_G(m);
+    int nj = 0;
+    int64_t off = 0;
+    for (int l = 0; l < m->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*m, l, &n, &k);
+        for (int kb = 0; kb < cdiv(k, H); ++kb) {
+            MGN_REQUIRE(nj < 12, "too many weight-gradient jobs");
+            a.job[nj].layer = l;
+            a.job[nj].kb = kb;
+            a.job[nj].n = n;
+            a.job[nj].k = k;
+            a.job[nj].w_off = off;
+            a.job[nj].b_off = kb == 0 ? off + (int64_t)n * k : -1;
+            ++nj;
+        }
+        off += (int64_t)n * k + n;
+    }
+    a.njobs = nj;
+    const int nchunks = (int)cdiv64(M, a.rows_per_chunk);
+    constexpr int LDT = 64 + 16 / sizeof(T);
+    const size_t lds = 2 * (size_t)H * LDT * sizeof(T);
+    auto fn = mlp_wgrad_kernel<T, H>;
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    if (nchunks > 0) {
+        ProfScope ps(PROF_WGRAD, st);
+        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
+        MGN_LAUNCH_CHECK();
+    }
+    ProfScope ps2(PROF_WGRAD_REDUCE, st);
+    const int NS = m->has_norm ? m->out_dim : 0;
+    const int64_t tot = a.G + NS;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv64(tot, MGN_THREADS)), dim3(MGN_THREADS), 0, st,
+                       (const float*)part, nchunks, a.G, dscale_part, ntiles, NS, grads);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
+    const size_t es = m->dtype == MGN_F32 ? 4 : 2;
+    const int BM = m->dtype == MGN_F32 ? 32 : 64;
+    const int64_t ntiles = cdiv64(M, BM);
+    const int64_t nchunks = cdiv64(M, wgrad_rows_per_chunk(m, M));
+    size_t b = align_up((size_t)m->n_layers * M * m->hidden * es);          // dz_save
+    b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
+    b += align_up((size_t)nchunks * grad_G(m) * sizeof(float));              // wgrad partial slabs
+    return b;
+}
+
+}  // namespace
+
+// =========================================================================== dispatch helpers
+#define MGN_DISPATCH_H(H_, ...)                                                          \
+    switch (H_) {                                                                        \
+        case 16: { constexpr int HH = 16; __VA_ARGS__; } break;                          \
+        case 32: { constexpr int HH = 32; __VA_ARGS__; } break;                          \
+        case 64: { constexpr int HH = 64; __VA_ARGS__; } break;                          \
+        case 128: { constexpr int HH = 128; __VA_ARGS__; } break;                        \
+        default: MGN_REQUIRE(false, "unsupported hidden size");                          \
+    }
+
+static int mlp_fwd_any(const mgn_mlp* m, int mode, const MlpIn& in, int64_t M, void* out, int out_dtype,
+                       int64_t out_ld, const void* resid, mgn_mlp_saved* sv, const mgn_topology* topo,
+                       const mgn_mlp* agg_mlp, const mgn_mlp_saved* agg_sv, void* agg_save, hipStream_t st) {
+    int rc = 0;
+#define MGN_F_CALL(T_, MODE_) rc = launch_fwd<T_, HH, MODE_>(m, in, M, out, out_dtype, out_ld, resid, sv, topo, agg_mlp, agg_sv, agg_save, st)
+    if (m->dtype == MGN_F32) {
+        if (mode == MODE_DENSE) { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(float, MODE_DENSE)) }
+        else if (mode == MODE_EDGE) { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(float, MODE_EDGE)) }
+        else { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(float, MODE_NODE)) }
+    } else {
+        if (mode == MODE_DENSE) { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(__bf16, MODE_DENSE)) }
+        else if (mode == MODE_EDGE) { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(__bf16, MODE_EDGE)) }
+        else { MGN_DISPATCH_H(m->hidden, MGN_F_CALL(__bf16, MODE_NODE)) }
+    }
+#undef MGN_F_CALL
+    return rc;
+}
+
+static int mlp_bwd_any(const mgn_mlp* m, int mode, int64_t M, const mgn_mlp_saved* sv, const void* dout,
+                       int dout_dtype, int64_t dout_ld, const BwdOut& o, void* dz, float* dsp, hipStream_t st) {
+    int rc = 0;
+#define MGN_B_CALL(T_, MODE_) rc = launch_bwd<T_, HH, MODE_>(m, M, sv, dout, dout_dtype, dout_ld, o, dz, dsp, st)
+    if (m->dtype == MGN_F32) {
+        if (mode == MODE_DENSE) { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(float, MODE_DENSE)) }
+        else if (mode == MODE_EDGE) { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(float, MODE_EDGE)) }
+        else { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(float, MODE_NODE)) }
+    } else {
+        if (mode == MODE_DENSE) { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(__bf16, MODE_DENSE)) }
+        else if (mode == MODE_EDGE) { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(__bf16, MODE_EDGE)) }
+        else { MGN_DISPATCH_H(m->hidden, MGN_B_CALL(__bf16, MODE_NODE)) }
+    }
+#undef MGN_B_CALL
+    return rc;
+}
+
+static int mlp_wgrad_any(const mgn_mlp* m, int64_t M, const MlpIn& in, const void* act, const void* dz,
+                         const float* dsp, int ntiles, float* part, float* grads, hipStream_t st) {
+    int rc = 0;
+    if (m->dtype == MGN_F32) {
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, in, act, dz, dsp, ntiles, part, grads, st)))
+    } else {
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, in, act, dz, dsp, ntiles, part, grads, st)))
+    }
+    return rc;
+}
+
+// Full backward of one MLP: data chain + weight grads. Workspace carve: dz | dscale | part.
+static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn& in, const mgn_mlp_saved* sv,
+                             const void* dout, int dout_dtype, int64_t dout_ld, const BwdOut& o, float* grads,
+                             void* ws, size_t ws_bytes, hipStream_t st) {
+    MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, M), "backward workspace too small");
+    const size_t es = m->dtype == MGN_F32 ? 4 : 2;
+    const int BM = m->dtype == MGN_F32 ? 32 : 64;
+    const int ntiles = (int)cdiv64(M, BM);
+    char* p = reinterpret_cast<char*>(ws);
+    void* dz = p;
+    p += align_up((size_t)m->n_layers * M * m->hidden * es);
+    float* dsp = reinterpret_cast<float*>(p);
+    p += align_up((size_t)ntiles * m->out_dim * sizeof(float));
+    float* part = reinterpret_cast<float*>(p);
+    if (M == 0) {
+        MGN_TRY(hipMemsetAsync(grads, 0, (grad_G(m) + (m->has_norm ? m->out_dim : 0)) * sizeof(float), st));
+        return 0;
+    }
+    if (int e = mlp_bwd_any(m, mode, M, sv, dout, dout_dtype, dout_ld, o, dz, dsp, st)) return e;
+    return mlp_wgrad_any(m, M, in, sv->act, dz, dsp, ntiles, part, grads, st);
+}
+
+// =========================================================================== node combine
+// dx[n] = dx_part[n] + Σ_{k in col seg n} dxij[k][0:H] + Σ_{j in row seg n} dxij[row_perm[j]][H:2H]
+template <class T, int H>
+__global__ __launch_bounds__(MGN_THREADS) void node_combine_kernel(const T* __restrict__ dx_part, const T* __restrict__ dxij,
+                                                                   const int32_t* __restrict__ col_ptr,
+                                                                   const int32_t* __restrict__ row_ptr,
+                                                                   const int32_t* __restrict__ row_perm, int64_t N,
+                                                                   T* __restrict__ dx) {
+    constexpr int CH = 16 / sizeof(T);
+    constexpr int LPN = H / CH;  // lanes per node
+    const int64_t gid = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x;
+    const int64_t n = gid / LPN;
+    const int c = (int)(gid % LPN) * CH;
+    if (n >= N) return;
+    float acc[CH], t[CH];
+    Chunk<T>::load(dx_part + n * H + c, acc);
+    for (int k = col_ptr[n]; k < col_ptr[n + 1]; ++k) {
+        Chunk<T>::load(dxij + (int64_t)k * 2 * H + c, t);
+#pragma unroll
+        for (int v = 0; v < CH; ++v) acc[v] += t[v];
+    }
+    for (int j = row_ptr[n]; j < row_ptr[n + 1]; ++j) {
+        Chunk<T>::load(dxij + (int64_t)row_perm[j] * 2 * H + H + c, t);
+#pragma unroll
+        for (int v = 0; v < CH; ++v) acc[v] += t[v];
+    }
+    Chunk<T>::store(dx + n * H + c, acc);
+}
+
+// =========================================================================== C ABI
+extern "C" {
+
+int64_t mgn_linear_pack_elems(int32_t n, int32_t k, int32_t dtype) { return linear_pack_elems(n, k, dtype); }
+
+int64_t mgn_mlp_pack_elems(const mgn_mlp* m) {
+    int64_t t = 0;
+    for (int l = 0; l < m->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*m, l, &n, &k);
+        t += linear_pack_elems(n, k, m->dtype);
+    }
+    return t;
+}
+
+int mgn_pack_weights(const mgn_pack_job* jobs, int32_t njobs, int64_t max_elems, mgn_stream_t stream) {
+    if (njobs <= 0) return 0;
+    MGN_REQUIRE(jobs != nullptr, "pack jobs NULL");
+    int64_t blocks = cdiv64(max_elems * 2, MGN_THREADS);  // packed size can exceed n*k (padding)
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
+    ProfScope ps(PROF_PACK, (hipStream_t)stream);
+    hipLaunchKernelGGL(pack_kernel<float>, dim3((unsigned)blocks, njobs), dim3(MGN_THREADS), 0, (hipStream_t)stream, jobs);
+    MGN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(pack_kernel<__bf16>, dim3((unsigned)blocks, njobs), dim3(MGN_THREADS), 0, (hipStream_t)stream, jobs);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
+                    int64_t rows, void* out, int32_t out_dtype, mgn_mlp_saved* saved, mgn_stream_t stream) {
+    if (int e = check_mlp(m)) return e;
+    MGN_REQUIRE(saved && saved->act && (!m->has_norm || (saved->z && saved->rden)), "saved buffers missing");
+    MGN_REQUIRE(in_dtype == MGN_F32 || in_dtype == m->dtype, "input dtype must be fp32 or the MLP dtype");
+    MlpIn mi;
+    memset(&mi, 0, sizeof(mi));
+    mi.seg[0] = SrcSeg{in, in_rows, in_ld, m->in_dim, in_dtype, 0, 0};
+    mi.nseg = 1;
+    return mlp_fwd_any(m, MODE_DENSE, mi, rows, out, out_dtype, m->out_dim, nullptr, saved, nullptr, nullptr,
+                       nullptr, nullptr, (hipStream_t)stream);
+}
+
+size_t mgn_mlp_backward_workspace_bytes(const mgn_mlp* m, int64_t rows) { return mlp_bwd_ws(m, rows); }
+
+int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
+                     int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,
+                     int32_t din_dtype, float* grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    if (int e = check_mlp(m)) return e;
+    MlpIn mi;
+    memset(&mi, 0, sizeof(mi));
+    mi.seg[0] = SrcSeg{in, in_rows, in_ld, m->in_dim, in_dtype, 0, 0};
+    mi.nseg = 1;
+    BwdOut o;
+    memset(&o, 0, sizeof(o));
+    o.mode = MODE_DENSE;
+    o.din = din;
+    o.din_dtype = din_dtype;
+    o.din_ld = m->in_dim;
+    return mlp_backward_impl(m, MODE_DENSE, rows, mi, saved, dout, dout_dtype, m->out_dim, o, grads, ws, ws_bytes,
+                             (hipStream_t)stream);
+}
+
+int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
+                      void* x_out, void* e_out, mgn_block_saved* saved, mgn_stream_t stream) {
+    if (int r = check_mlp(edge)) return r;
+    if (int r = check_mlp(node)) return r;
+    const int H = edge->hidden;
+    MGN_REQUIRE(edge->in_dim == 3 * H && edge->out_dim == H, "edge MLP must be 3h -> h");
+    MGN_REQUIRE(node->in_dim == 2 * H && node->out_dim == H && node->hidden == H, "node MLP must be 2h -> h");
+    MGN_REQUIRE(saved->edge.z && saved->edge.rden && saved->aggr, "block saved buffers missing");
+    MGN_REQUIRE(edge->dtype == node->dtype, "edge/node MLP dtype mismatch");
+    hipStream_t st = (hipStream_t)stream;
+    const int dt = edge->dtype;
+    MlpIn ein;
+    memset(&ein, 0, sizeof(ein));
+    ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
+    ein.seg[1] = SrcSeg{x, t->csc_dst, H, H, dt, H, 0};
+    ein.seg[2] = SrcSeg{x, t->csc_src, H, H, dt, 2 * H, 0};
+    ein.nseg = 3;
+    if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr, nullptr,
+                            nullptr, st))
+        return r;
+    MlpIn nin;
+    memset(&nin, 0, sizeof(nin));
+    nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
+    nin.nseg = 1;
+    // K0 = 2H: the aggregation fills columns [H, 2H) inside the kernel
+    return mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
+                       saved->aggr, st);
+}
+
+static size_t block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, size_t* off_mlp,
+                             size_t* off_dxpart, size_t* off_daggr, size_t* off_dxij) {
+    const size_t es = edge->dtype == MGN_F32 ? 4 : 2;
+    const int H = edge->hidden;
+    size_t mlp_ws = mlp_bwd_ws(edge, t->num_edges);
+    const size_t nws = mlp_bwd_ws(node, t->num_nodes);
+    if (nws > mlp_ws) mlp_ws = nws;
+    size_t o = 0;
+    *off_mlp = o;
+    o += align_up(mlp_ws);
+    *off_dxpart = o;
+    o += align_up((size_t)t->num_nodes * H * es);
+    *off_daggr = o;
+    o += align_up((size_t)t->num_nodes * H * es);
+    *off_dxij = o;
+    o += align_up((size_t)t->num_edges * 2 * H * es);
+    return o;
+}
+
+size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    size_t a, b, c, d;
+    return block_ws_parts(t, edge, node, &a, &b, &c, &d);
+}
+
+int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
+                       const mgn_block_saved* saved, const void* dx_out, const void* de_out, void* dx, void* de,
+                       float* edge_grads, float* node_grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    if (int r = check_mlp(edge)) return r;
+    if (int r = check_mlp(node)) return r;
+    size_t o_mlp, o_dxp, o_dag, o_dij;
+    const size_t need = block_ws_parts(t, edge, node, &o_mlp, &o_dxp, &o_dag, &o_dij);
+    MGN_REQUIRE(ws_bytes >= need, "block backward workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const int H = edge->hidden, dt = edge->dtype;
+    char* w = reinterpret_cast<char*>(ws);
+    void* mlp_ws = w + o_mlp;
+    void* dx_part = w + o_dxp;
+    void* d_aggr = w + o_dag;
+    void* dxij = w + o_dij;
+    const size_t mlp_ws_bytes = o_dxp - o_mlp;
+
+    // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
+    MlpIn nin;
+    memset(&nin, 0, sizeof(nin));
+    nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
+    nin.seg[1] = SrcSeg{saved->aggr, nullptr, H, H, dt, H, 0};
+    nin.nseg = 2;
+    BwdOut on;
+    memset(&on, 0, sizeof(on));
+    on.mode = MODE_NODE;
+    on.o1 = dx_part;
+    on.o2 = d_aggr;
+    if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on, node_grads,
+                                  mlp_ws, mlp_ws_bytes, st))
+        return r;
+    // edge MLP: dY = de_out + d_aggr[dst] -> de = de_out + dA0[:, :H], dxij = dA0[:, H:3H]
+    MlpIn ein;
+    memset(&ein, 0, sizeof(ein));
+    ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
+    ein.seg[1] = SrcSeg{x, t->csc_dst, H, H, dt, H, 0};
+    ein.seg[2] = SrcSeg{x, t->csc_src, H, H, dt, 2 * H, 0};
+    ein.nseg = 3;
+    BwdOut oe;
+    memset(&oe, 0, sizeof(oe));
+    oe.mode = MODE_EDGE;
+    oe.gath = d_aggr;
+    oe.gath_idx = t->csc_dst;
+    oe.o1 = de;
+    oe.o2 = dxij;
+    if (int r = mlp_backward_impl(edge, MODE_EDGE, t->num_edges, ein, &saved->edge, de_out, dt, H, oe, edge_grads,
+                                  mlp_ws, mlp_ws_bytes, st))
+        return r;
+    // dx = dx_part + Σ_col dxi + Σ_row dxj
+    const int64_t N = t->num_nodes;
+    if (N == 0) return 0;
+    const int lpn = H / (int)(16 / (dt == MGN_F32 ? 4 : 2));
+    const unsigned blocks = (unsigned)cdiv64(N * lpn, MGN_THREADS);
+    ProfScope ps(PROF_COMBINE, st);
+    if (dt == MGN_F32) {
+        MGN_DISPATCH_H(H, hipLaunchKernelGGL((node_combine_kernel<float, HH>), dim3(blocks), dim3(MGN_THREADS), 0, st,
+                                             (const float*)dx_part, (const float*)dxij, t->col_ptr, t->row_ptr,
+                                             t->row_perm, N, (float*)dx))
+    } else {
+        MGN_DISPATCH_H(H, hipLaunchKernelGGL((node_combine_kernel<__bf16, HH>), dim3(blocks), dim3(MGN_THREADS), 0,
+                                             st, (const __bf16*)dx_part, (const __bf16*)dxij, t->col_ptr, t->row_ptr,
+                                             t->row_perm, N, (__bf16*)dx))
+    }
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+"""ctypes binding of libmgn (include/mgn.h) — the MI355X-native hot path.
+
+The library is built in-tree by `python __graft_entry__.py` (hipcc --offload-arch=gfx950) into
+graph-physics_amd/graphphysics/_lib/libmgn.so. There is NO fallback: every model entry point
+raises if the library or a HIP device is missing.
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
+
+MGN_F32 = 0
+MGN_BF16 = 1
+MGN_MAX_LAYERS = 8
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_sz = ctypes.c_size_t
+_dbl = ctypes.c_double
+
+
+class Topology(ctypes.Structure):
+    _fields_ = [("num_nodes", _i64), ("num_edges", _i64), ("csc_src", _vp), ("csc_dst", _vp),
+                ("csc_eid", _vp), ("col_ptr", _vp), ("row_ptr", _vp), ("row_perm", _vp)]
+
+
+class Mlp(ctypes.Structure):
+    _fields_ = [("n_layers", _i32), ("in_dim", _i32), ("hidden", _i32), ("out_dim", _i32),
+                ("has_norm", _i32), ("dtype", _i32), ("wpack", _vp), ("wtpack", _vp),
+                ("bias", _vp * MGN_MAX_LAYERS), ("scale", _vp)]
+
+
+class MlpSaved(ctypes.Structure):
+    _fields_ = [("act", _vp), ("z", _vp), ("rden", _vp)]
+
+
+class BlockSaved(ctypes.Structure):
+    _fields_ = [("edge", MlpSaved), ("node", MlpSaved), ("aggr", _vp)]
+
+
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", _vp), ("dst", _vp), ("dstT", _vp), ("n", _i32), ("k", _i32),
+                ("dtype", _i32), ("reserved", _i32)]
+
+
+EXPORTS = {
+    "mgn_abi_version": (_i32, []),
+    "mgn_last_error": (ctypes.c_char_p, []),
+    "mgn_topology_workspace_bytes": (_sz, [_i64, _i64]),
+    "mgn_topology_build": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_linear_pack_elems": (_i64, [_i32, _i32, _i32]),
+    "mgn_mlp_pack_elems": (_i64, [ctypes.POINTER(Mlp)]),
+    "mgn_pack_weights": (_i32, [_vp, _i32, _i64, _vp]),
+    "mgn_mlp_forward": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64, _vp, _i32,
+                               ctypes.POINTER(MlpSaved), _vp]),
+    "mgn_mlp_backward_workspace_bytes": (_sz, [ctypes.POINTER(Mlp), _i64]),
+    "mgn_mlp_backward": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
+                                ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp]),
+    "mgn_block_forward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                 _vp, _vp, _vp, _vp, ctypes.POINTER(BlockSaved), _vp]),
+    "mgn_block_backward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
+                                                 ctypes.POINTER(Mlp)]),
+    "mgn_block_backward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                  _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _sz, _vp]),
+    "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
+    "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
+    "mgn_profile_enable": (_i32, [_i32]),
+    "mgn_profile_collect": (_i32, [_i32, _vp, _vp]),
+}
+
+PROF_KINDS = ["fwd_edge", "fwd_node", "fwd_dense", "bwd_edge", "bwd_node", "bwd_dense", "wgrad",
+              "wgrad_reduce", "combine", "pack", "adamw"]
+
+
+def profile_enable(on=True):
+    check(lib().mgn_profile_enable(int(on)))
+
+
+def profile_collect():
+    """{kernel class: (total_ms, launches)} since the last profile_enable()."""
+    out = {}
+    for i, name in enumerate(PROF_KINDS):
+        ms, cnt = ctypes.c_double(), ctypes.c_int64()
+        check(lib().mgn_profile_collect(i, ctypes.byref(ms), ctypes.byref(cnt)))
+        out[name] = (ms.value, cnt.value)
+    return out
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libmgn and bind every exported symbol (no device needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libmgn not built ({path} missing): run `python __graft_entry__.py` (hipcc gfx950). "
+            "The MGN path has no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().mgn_last_error().decode(errors="replace")
+        if "out of range" in msg:
+            raise IndexError(msg)
+        raise RuntimeError(f"libmgn error {rc}: {msg}")
+
+
+def require_device(t):
+    if not t.is_cuda:
+        raise RuntimeError("the MI355X MGN path needs tensors on a HIP device (no CPU fallback)")
+
+
+def stream_ptr(device=None):
+    return _vp(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    """Device address of a tensor (None -> NULL; raw ints / c_void_p pass through)."""
+    if t is None:
+        return _vp(0)
+    if isinstance(t, _vp):
+        return t
+    if isinstance(t, int):
+        return _vp(t)
+    return _vp(t.data_ptr())
+
+
+def mgn_dtype(torch_dtype):
+    if torch_dtype == torch.float32:
+        return MGN_F32
+    if torch_dtype == torch.bfloat16:
+        return MGN_BF16
+    raise ValueError(f"unsupported compute dtype {torch_dtype}")
+
+
+def torch_dtype(mdt):
+    return torch.float32 if mdt == MGN_F32 else torch.bfloat16

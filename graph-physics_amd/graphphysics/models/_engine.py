@@ -1,0 +1,455 @@
+"""Execution engine: drives libmgn (include/mgn.h) from PyTorch autograd.
+
+* GraphTopology  — target-sorted edge order + segment pointers for an edge_index (built on device
+                   by mgn_topology_build, cached per edge_index tensor object).
+* MlpSpec        — one build_mlp nn.Sequential (reference graphphysics/models/layers.py:77-113)
+                   seen by the kernels: its Linear weights are packed into MFMA fragments, biases and
+                   RMSNorm scale are read straight from the fp32 master parameters.
+* ModelPlan      — every MLP of a module in parameter-registration order; one pack launch per
+                   forward; gradients land in ONE flat fp32 buffer laid out exactly like
+                   module.parameters() (so data-parallel all-reduce and the fused optimizer each
+                   touch one contiguous buffer).
+* EPDFunction / BlockFunction — torch.autograd.Function wrappers of EncodeProcessDecode.forward
+                   (processors.py:111-137) and GraphNetBlock.forward (layers.py:667-701).
+Device memory is always allocated here through the PyTorch caching allocator; the library owns
+none. No CPU fallback exists: tensors must live on a HIP device.
+"""
+import ctypes
+import weakref
+
+import torch
+import torch.nn as nn
+
+from graphphysics import _native as nat
+
+
+# --------------------------------------------------------------------------- topology
+class GraphTopology:
+    def __init__(self, edge_index, num_nodes):
+        nat.require_device(edge_index)
+        L = nat.lib()
+        ei = edge_index.to(torch.int64).contiguous()
+        if ei.dim() != 2 or ei.shape[0] != 2:
+            raise ValueError("edge_index must have shape [2, E]")
+        E, N = int(ei.shape[1]), int(num_nodes)
+        dev = ei.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.num_nodes, self.num_edges, self.device = N, E, dev
+        self.csc_src = torch.empty(max(E, 1), **i32)
+        self.csc_dst = torch.empty(max(E, 1), **i32)
+        self.csc_eid = torch.empty(max(E, 1), **i32)
+        self.row_perm = torch.empty(max(E, 1), **i32)
+        self.col_ptr = torch.empty(N + 1, **i32)
+        self.row_ptr = torch.empty(N + 1, **i32)
+        wsb = L.mgn_topology_workspace_bytes(E, N)
+        ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
+        nat.check(L.mgn_topology_build(
+            nat.ptr(ei), E, N, nat.ptr(self.csc_src), nat.ptr(self.csc_dst), nat.ptr(self.csc_eid),
+            nat.ptr(self.col_ptr), nat.ptr(self.row_ptr), nat.ptr(self.row_perm), nat.ptr(ws), wsb,
+            nat.stream_ptr(dev)))
+        self.struct = nat.Topology(N, E, self.csc_src.data_ptr(), self.csc_dst.data_ptr(),
+                                   self.csc_eid.data_ptr(), self.col_ptr.data_ptr(),
+                                   self.row_ptr.data_ptr(), self.row_perm.data_ptr())
+
+
+_TOPO_CACHE = []  # [(weakref(edge_index), version, num_nodes, topo)], most recent first
+_TOPO_CACHE_MAX = 8
+
+
+def get_topology(edge_index, num_nodes):
+    """Topology for this exact edge_index tensor object (identity + version checked: a freed
+    tensor's address reused by a new one never hits a stale entry)."""
+    for i, (ref, ver, n, topo) in enumerate(_TOPO_CACHE):
+        if ref() is edge_index and ver == edge_index._version and n == num_nodes:
+            if i:
+                _TOPO_CACHE.insert(0, _TOPO_CACHE.pop(i))
+            return topo
+    topo = GraphTopology(edge_index, num_nodes)
+    _TOPO_CACHE.insert(0, (weakref.ref(edge_index), edge_index._version, num_nodes, topo))
+    del _TOPO_CACHE[_TOPO_CACHE_MAX:]
+    return topo
+
+
+# --------------------------------------------------------------------------- MLPs and plans
+class MlpSpec:
+    def __init__(self, seq):
+        from graphphysics.models.layers import RMSNorm
+
+        mods = list(seq)
+        linears = [m for m in mods if isinstance(m, nn.Linear)]
+        norm = [m for m in mods if isinstance(m, RMSNorm)]
+        expect = []
+        for i in range(len(linears)):
+            expect.append(nn.Linear)
+            if i < len(linears) - 1:
+                expect.append(nn.ReLU)
+        if norm:
+            expect.append(RMSNorm)
+        if [type(m) for m in mods] != expect or len(norm) > 1:
+            raise ValueError("MLP must be Linear,ReLU,...,Linear[,RMSNorm] (reference build_mlp)")
+        if norm and (norm[0].bias or not (norm[0].p < 0.0 or norm[0].p > 1.0) or norm[0].eps != 1e-8):
+            raise ValueError("fused RMSNorm supports the reference defaults (p=-1, eps=1e-8, no bias)")
+        self.linears = linears
+        self.norm = norm[0] if norm else None
+        self.n_layers = len(linears)
+        self.in_dim = linears[0].in_features
+        self.hidden = linears[0].out_features
+        self.out_dim = linears[-1].out_features
+        self.params = [p for lin in linears for p in (lin.weight, lin.bias)]
+        if self.norm is not None:
+            self.params.append(self.norm.scale)
+        self.numel = sum(p.numel() for p in self.params)
+
+    def describe(self, mdt, wpack, wtpack):
+        d = nat.Mlp()
+        d.n_layers, d.in_dim, d.hidden, d.out_dim = self.n_layers, self.in_dim, self.hidden, self.out_dim
+        d.has_norm, d.dtype = int(self.norm is not None), mdt
+        d.wpack, d.wtpack = wpack, wtpack
+        for i, lin in enumerate(self.linears):
+            d.bias[i] = lin.bias.data_ptr()
+        d.scale = self.norm.scale.data_ptr() if self.norm is not None else 0
+        return d
+
+
+class _PackedWeights:
+    """Fragment-packed copies of all Linear weights of a plan for one (device, dtype)."""
+
+    def __init__(self, plan, device, mdt):
+        L = nat.lib()
+        tdt = nat.torch_dtype(mdt)
+        regions, jobs, total, max_el = [], [], 0, 1
+        for spec in plan.specs:
+            per = [int(L.mgn_linear_pack_elems(lin.out_features, lin.in_features, mdt))
+                   for lin in spec.linears]
+            regions.append((total, per))
+            total += 2 * sum(per)
+        self.buf = torch.empty(max(total, 1), dtype=tdt, device=device)
+        esz = self.buf.element_size()
+        base = self.buf.data_ptr()
+        self.descs = []
+        for spec, (off, per) in zip(plan.specs, regions):
+            n = sum(per)
+            wp, wtp = base + off * esz, base + (off + n) * esz
+            o = 0
+            for lin, cnt in zip(spec.linears, per):
+                j = nat.PackJob(lin.weight.data_ptr(), wp + o * esz, wtp + o * esz,
+                                lin.out_features, lin.in_features, mdt, 0)
+                jobs.append(j)
+                max_el = max(max_el, lin.out_features * lin.in_features)
+                o += cnt
+            self.descs.append(spec.describe(mdt, wp, wtp))
+        arr = (nat.PackJob * len(jobs))(*jobs)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.jobs = raw.to(device)
+        self.njobs, self.max_el = len(jobs), max_el
+        self.wptrs = tuple(lin.weight.data_ptr() for s in plan.specs for lin in s.linears)
+
+    def repack(self, stream):
+        nat.check(nat.lib().mgn_pack_weights(nat.ptr(self.jobs), self.njobs, self.max_el, stream))
+
+
+class ModelPlan:
+    """All MLPs of a module, in module.parameters() order."""
+
+    def __init__(self, module, mlps):
+        self.module = module
+        self.specs = [MlpSpec(m) for m in mlps]
+        order = [p for s in self.specs for p in s.params]
+        mine = list(module.parameters())
+        if len(order) != len(mine) or any(a is not b for a, b in zip(order, mine)):
+            raise RuntimeError("module parameters are not exactly its MLP parameters in order")
+        self.params = mine
+        self.offsets = []
+        o = 0
+        for s in self.specs:
+            self.offsets.append(o)
+            o += s.numel
+        self.numel = o
+        self._packed = {}
+
+    def packed(self, device, mdt):
+        key = (str(device), mdt)
+        pw = self._packed.get(key)
+        wptrs = tuple(lin.weight.data_ptr() for s in self.specs for lin in s.linears)
+        if pw is None or pw.wptrs != wptrs:
+            pw = _PackedWeights(self, device, mdt)
+            self._packed[key] = pw
+        return pw
+
+    def grad_views(self, flat):
+        out, o = [], 0
+        for p in self.params:
+            n = p.numel()
+            out.append(flat[o:o + n].view_as(p))
+            o += n
+        return out
+
+
+def flatten_parameters(module):
+    """Re-home every parameter as a view of ONE contiguous fp32 buffer (registration order), so
+    the fused optimizer and the gradient all-reduce each see a single buffer."""
+    params = list(module.parameters())
+    if not params:
+        return None
+    dev = params[0].device
+    if any(p.device != dev or p.dtype != torch.float32 for p in params):
+        return None
+    flat = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=dev)
+    o = 0
+    with torch.no_grad():
+        for p in params:
+            n = p.numel()
+            flat[o:o + n].copy_(p.reshape(-1))
+            p.data = flat[o:o + n].view_as(p)
+            o += n
+    module._flat_params = flat
+    return flat
+
+
+# --------------------------------------------------------------------------- helpers
+def _empty(n, dtype, device):
+    return torch.empty(max(int(n), 1), dtype=dtype, device=device)
+
+
+def _alloc_mlp_saved(spec, rows, tdt, device, need_z):
+    act = _empty((spec.n_layers - 1) * rows * spec.hidden, tdt, device)
+    z = _empty(rows * spec.hidden, tdt, device) if need_z else None
+    rden = _empty(rows, torch.float32, device) if need_z else None
+    s = nat.MlpSaved(act.data_ptr(), z.data_ptr() if z is not None else 0,
+                     rden.data_ptr() if rden is not None else 0)
+    return s, (act, z, rden)
+
+
+def _alloc_block_saved(espec, nspec, topo, tdt, device):
+    se, ke = _alloc_mlp_saved(espec, topo.num_edges, tdt, device, True)
+    sn, kn = _alloc_mlp_saved(nspec, topo.num_nodes, tdt, device, nspec.norm is not None)
+    aggr = _empty(topo.num_nodes * espec.hidden, tdt, device)
+    return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
+
+
+def _permute(src, idx, rows, cols, in_mdt, out_tdt, scatter, stream, out=None):
+    if out is None:
+        out = torch.empty((rows, cols), dtype=out_tdt, device=src.device)
+    nat.check(nat.lib().mgn_permute_rows(nat.ptr(src), nat.ptr(out), nat.ptr(idx), rows, cols, in_mdt,
+                                         nat.mgn_dtype(out_tdt), int(scatter), stream))
+    return out
+
+
+def _mlp_fwd(desc, spec, inp, in_mdt, in_ld, rows_idx, rows, out, out_mdt, saved, stream):
+    nat.check(nat.lib().mgn_mlp_forward(ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld,
+                                        nat.ptr(rows_idx), rows, nat.ptr(out), out_mdt,
+                                        ctypes.byref(saved), stream))
+
+
+def _mlp_bwd(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws,
+             stream):
+    nat.check(nat.lib().mgn_mlp_backward(
+        ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld, nat.ptr(rows_idx), rows, ctypes.byref(saved),
+        nat.ptr(dout), dout_mdt, nat.ptr(din), din_mdt, nat.ptr(grads), nat.ptr(ws),
+        ws.numel() if ws is not None else 0, stream))
+
+
+def _ws_bytes_mlp(desc, rows):
+    return int(nat.lib().mgn_mlp_backward_workspace_bytes(ctypes.byref(desc), rows))
+
+
+def _ws_bytes_block(topo, de, dn):
+    return int(nat.lib().mgn_block_backward_workspace_bytes(ctypes.byref(topo.struct),
+                                                            ctypes.byref(de), ctypes.byref(dn)))
+
+
+# --------------------------------------------------------------------------- EncodeProcessDecode
+class EPDFunction(torch.autograd.Function):
+    """y = EncodeProcessDecode(graph) with the whole processor on libmgn.
+    Encoders: specs[0] (nodes), specs[1] (edges); decoder specs[2]; blocks: specs[3+2b],
+    specs[4+2b]. only_processor: specs are the blocks only."""
+
+    @staticmethod
+    def forward(ctx, plan, mdt, only_processor, x, edge_attr, topo, *params):
+        dev = x.device
+        st = nat.stream_ptr(dev)
+        tdt = nat.torch_dtype(mdt)
+        pw = plan.packed(dev, mdt)
+        pw.repack(st)
+        descs = pw.descs
+        N, E = topo.num_nodes, topo.num_edges
+        train = any(ctx.needs_input_grad)
+        if only_processor:
+            bspecs, bdescs = plan.specs, descs
+            H = bspecs[0].hidden
+            x0 = x.detach().to(tdt).contiguous()
+            e0 = _permute(edge_attr.detach().float().contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt,
+                          False, st)
+            sv_ne = sv_ee = sv_dec = None
+            xin = ein = None
+        else:
+            bspecs, bdescs = plan.specs[3:], descs[3:]
+            ne, ee, dec = plan.specs[:3]
+            H = ne.hidden
+            xin = x.detach().float().contiguous()
+            ein = edge_attr.detach().float().contiguous()
+            x0 = torch.empty((N, H), dtype=tdt, device=dev)
+            e0 = torch.empty((E, H), dtype=tdt, device=dev)
+            sv_ne = _alloc_mlp_saved(ne, N, tdt, dev, ne.norm is not None)
+            sv_ee = _alloc_mlp_saved(ee, E, tdt, dev, ee.norm is not None)
+            _mlp_fwd(descs[0], ne, xin, nat.MGN_F32, ne.in_dim, None, N, x0, mdt, sv_ne[0], st)
+            _mlp_fwd(descs[1], ee, ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, e0, mdt, sv_ee[0], st)
+        xs, es, svs = [x0], [e0], []
+        nb = len(bspecs) // 2
+        scratch = None
+        for b in range(nb):
+            es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
+            if train or scratch is None:
+                sv = _alloc_block_saved(es_, ns_, topo, tdt, dev)
+                if not train:
+                    scratch = sv
+            else:
+                sv = scratch
+            x1 = torch.empty((N, H), dtype=tdt, device=dev)
+            e1 = torch.empty((E, H), dtype=tdt, device=dev)
+            nat.check(nat.lib().mgn_block_forward(
+                ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
+                nat.ptr(xs[-1]), nat.ptr(es[-1]), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), st))
+            if train:
+                xs.append(x1)
+                es.append(e1)
+                svs.append(sv)
+            else:
+                xs, es = [x1], [e1]
+        if only_processor:
+            out = xs[-1].float()
+        else:
+            out = torch.empty((N, dec.out_dim), dtype=torch.float32, device=dev)
+            sv_dec = _alloc_mlp_saved(dec, N, tdt, dev, dec.norm is not None)
+            _mlp_fwd(descs[2], dec, xs[-1], mdt, H, None, N, out, nat.MGN_F32, sv_dec[0], st)
+        if train:
+            ctx.plan, ctx.mdt, ctx.only_processor, ctx.topo = plan, mdt, only_processor, topo
+            ctx.pw = pw
+            ctx.state = (xin, ein, xs, es, svs, sv_ne, sv_ee, sv_dec)
+            ctx.H = H
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        plan, mdt, topo, pw = ctx.plan, ctx.mdt, ctx.topo, ctx.pw
+        xin, ein, xs, es, svs, sv_ne, sv_ee, sv_dec = ctx.state
+        dev = xs[0].device
+        st = nat.stream_ptr(dev)
+        tdt = nat.torch_dtype(mdt)
+        N, E, H = topo.num_nodes, topo.num_edges, ctx.H
+        descs = pw.descs
+        G = torch.empty(plan.numel, dtype=torch.float32, device=dev)
+        gp = G.data_ptr()
+        off = plan.offsets
+        if ctx.only_processor:
+            bdescs, boff = descs, off
+        else:
+            bdescs, boff = descs[3:], off[3:]
+        need = _ws_bytes_block(topo, bdescs[0], bdescs[1]) if len(bdescs) >= 2 else 0
+        if not ctx.only_processor:
+            need = max(need, _ws_bytes_mlp(descs[0], N), _ws_bytes_mlp(descs[1], E),
+                       _ws_bytes_mlp(descs[2], N))
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        if ctx.only_processor:
+            dx = gout.detach().to(tdt).contiguous()
+        else:
+            dx = torch.empty((N, H), dtype=tdt, device=dev)
+            g = gout.detach().float().contiguous()
+            _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
+                     ctypes.c_void_p(gp + 4 * off[2]), ws, st)
+        de = torch.zeros((E, H), dtype=tdt, device=dev)
+        nb = len(bdescs) // 2
+        for b in reversed(range(nb)):
+            dx1 = torch.empty((N, H), dtype=tdt, device=dev)
+            de1 = torch.empty((E, H), dtype=tdt, device=dev)
+            nat.check(nat.lib().mgn_block_backward(
+                ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
+                nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
+                nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
+                ctypes.c_void_p(gp + 4 * boff[2 * b + 1]), nat.ptr(ws), ws.numel(), st))
+            dx, de = dx1, de1
+        gx = gea = None
+        nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        if ctx.only_processor:
+            if nx:
+                gx = dx.float()
+            if nea:
+                gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)
+        else:
+            ne, ee = plan.specs[0], plan.specs[1]
+            gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
+            _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
+                     ctypes.c_void_p(gp + 4 * off[0]), ws, st)
+            gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
+            _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                     nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
+            gx = gxc
+            if nea:
+                gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
+        ctx.state = None
+        return (None, None, None, gx, gea, None, *plan.grad_views(G))
+
+
+# --------------------------------------------------------------------------- GraphNetBlock
+class BlockFunction(torch.autograd.Function):
+    """(x', e') = GraphNetBlock(x, edge_index, e) with edges in the CALLER's order."""
+
+    @staticmethod
+    def forward(ctx, plan, mdt, x, edge_attr, topo, *params):
+        dev = x.device
+        st = nat.stream_ptr(dev)
+        tdt = nat.torch_dtype(mdt)
+        pw = plan.packed(dev, mdt)
+        pw.repack(st)
+        espec, nspec = plan.specs
+        H = espec.hidden
+        N, E = topo.num_nodes, topo.num_edges
+        x0 = x.detach().to(tdt).contiguous()
+        e0 = _permute(edge_attr.detach().contiguous(), topo.csc_eid, E, H,
+                      nat.mgn_dtype(edge_attr.dtype) if edge_attr.dtype in (torch.float32, torch.bfloat16)
+                      else nat.MGN_F32, tdt, False, st) if E else torch.empty((0, H), dtype=tdt, device=dev)
+        sv = _alloc_block_saved(espec, nspec, topo, tdt, dev)
+        x1 = torch.empty((N, H), dtype=tdt, device=dev)
+        e1 = torch.empty((max(E, 1), H), dtype=tdt, device=dev)
+        nat.check(nat.lib().mgn_block_forward(
+            ctypes.byref(topo.struct), ctypes.byref(pw.descs[0]), ctypes.byref(pw.descs[1]), nat.ptr(x0),
+            nat.ptr(e0), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), st))
+        e_out = _permute(e1, topo.csc_eid, E, H, mdt, x.dtype, True, st) if E else \
+            torch.empty((0, H), dtype=x.dtype, device=dev)
+        if any(ctx.needs_input_grad):
+            ctx.plan, ctx.mdt, ctx.topo, ctx.pw = plan, mdt, topo, pw
+            ctx.state = (x0, e0, sv)
+            ctx.xdtype = x.dtype
+        return x1.to(x.dtype), e_out
+
+    @staticmethod
+    def backward(ctx, gx, ge):
+        plan, mdt, topo, pw = ctx.plan, ctx.mdt, ctx.topo, ctx.pw
+        x0, e0, sv = ctx.state
+        dev = x0.device
+        st = nat.stream_ptr(dev)
+        tdt = nat.torch_dtype(mdt)
+        N, E = topo.num_nodes, topo.num_edges
+        H = plan.specs[0].hidden
+        dxo = (gx if gx is not None else torch.zeros((N, H), device=dev)).detach().to(tdt).contiguous()
+        if ge is None or E == 0:
+            deo = torch.zeros((max(E, 1), H), dtype=tdt, device=dev)
+        else:
+            deo = _permute(ge.detach().float().contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt, False, st)
+        G = torch.empty(plan.numel, dtype=torch.float32, device=dev)
+        ws = torch.empty(max(_ws_bytes_block(topo, pw.descs[0], pw.descs[1]), 1), dtype=torch.uint8,
+                         device=dev)
+        dx = torch.empty((N, H), dtype=tdt, device=dev)
+        de = torch.empty((max(E, 1), H), dtype=tdt, device=dev)
+        nat.check(nat.lib().mgn_block_backward(
+            ctypes.byref(topo.struct), ctypes.byref(pw.descs[0]), ctypes.byref(pw.descs[1]), nat.ptr(x0),
+            nat.ptr(e0), ctypes.byref(sv[0]), nat.ptr(dxo), nat.ptr(deo), nat.ptr(dx), nat.ptr(de),
+            ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(G.data_ptr() + 4 * plan.offsets[1]),
+            nat.ptr(ws), ws.numel(), st))
+        gxo = dx.to(ctx.xdtype) if ctx.needs_input_grad[2] else None
+        geo = None
+        if ctx.needs_input_grad[3]:
+            geo = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st) if E else \
+                torch.zeros((0, H), device=dev)
+        ctx.state = None
+        return (None, None, gxo, geo, None, *plan.grad_views(G))

@@ -1,0 +1,105 @@
+"""Drop-in Simulator (reference graphphysics/models/simulator.py:128-405) for the MGN path.
+
+Same constructor, attributes and forward contract: forward(inputs) ->
+(network_output, target_delta_normalized, outputs-or-None). The per-step preamble (target delta,
+one-hot node type, three online Normalizers) is O(N+E) element-wise torch work on the device; the
+Normalizers never synchronise with the host. The wrapped model is the libmgn
+EncodeProcessDecode. GMM sampling (num_mixture_components > 0) is out of scope.
+"""
+import os
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from graphphysics.models.layers import Normalizer
+from graphphysics.utils.data import Data
+from graphphysics.utils.nodetype import NodeType
+
+
+class Simulator(nn.Module):
+    def __init__(self, node_input_size: int, edge_input_size: int, output_size: int,
+                 feature_index_start: int, feature_index_end: int, output_index_start: int,
+                 output_index_end: int, node_type_index: int, model: nn.Module,
+                 device: torch.device, model_dir: str = "checkpoint/simulator.pth"):
+        super().__init__()
+        self.node_input_size = node_input_size
+        self.edge_input_size = edge_input_size if edge_input_size > 0 else None
+        self.output_size = output_size
+        self.feature_index_start, self.feature_index_end = feature_index_start, feature_index_end
+        self.node_type_index = node_type_index
+        self.output_index_start, self.output_index_end = output_index_start, output_index_end
+        self.model_dir = model_dir
+        self.model = model.to(device)
+        self._output_normalizer = Normalizer(size=output_size, name="output_normalizer", device=device)
+        self._node_normalizer = Normalizer(size=node_input_size, name="node_normalizer", device=device)
+        self._edge_normalizer = (Normalizer(size=edge_input_size, name="edge_normalizer", device=device)
+                                 if self.edge_input_size is not None else None)
+        self.device = device
+
+    # ---- data-parallel hook: all-reduce batch statistics across graph shards
+    def set_process_group(self, group):
+        for n in (self._output_normalizer, self._node_normalizer, self._edge_normalizer):
+            if n is not None:
+                n.process_group = group
+
+    def _get_pre_target(self, inputs) -> torch.Tensor:
+        return inputs.x[:, self.output_index_start:self.output_index_end]
+
+    def _get_target_normalized(self, inputs, is_training: bool = True) -> torch.Tensor:
+        delta = inputs.y - self._get_pre_target(inputs)
+        return self._output_normalizer(delta, is_training)
+
+    def _get_one_hot_type(self, inputs) -> torch.Tensor:
+        node_type = inputs.x[:, self.node_type_index]
+        return torch.nn.functional.one_hot(torch.squeeze(node_type.long()), NodeType.SIZE)
+
+    def _build_node_features(self, inputs, one_hot_type: torch.Tensor) -> torch.Tensor:
+        feats = inputs.x[:, self.feature_index_start:self.feature_index_end]
+        return torch.cat([feats, one_hot_type], dim=1)
+
+    def _build_input_graph(self, inputs, is_training: bool) -> Tuple[Data, torch.Tensor]:
+        tdn = self._get_target_normalized(inputs, is_training)
+        nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
+        nfn = self._node_normalizer(nf, is_training)
+        ea = (self._edge_normalizer(inputs.edge_attr, is_training) if self._edge_normalizer is not None
+              else inputs.edge_attr)
+        graph = Data(x=nfn, pos=getattr(inputs, "pos", None), edge_attr=ea, edge_index=inputs.edge_index)
+        return graph, tdn
+
+    def _build_outputs(self, inputs, network_output: torch.Tensor) -> torch.Tensor:
+        return self._get_pre_target(inputs) + self._output_normalizer.inverse(network_output)
+
+    def forward(self, inputs) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+        graph, tdn = self._build_input_graph(inputs=inputs, is_training=self.training)
+        net = self.model(graph)
+        if self.training:
+            return net, tdn, None
+        if self.model.K != 0:
+            raise NotImplementedError("GMM sampling is outside the MI355X MGN hot path")
+        return net, tdn, self._build_outputs(inputs=inputs, network_output=net)
+
+    def freeze_all(self) -> None:
+        for p in self.model.parameters():
+            p.requires_grad = False
+
+    def load_checkpoint(self, ckpdir: Optional[str] = None) -> None:
+        ckpdir = ckpdir or self.model_dir
+        ck = torch.load(ckpdir, map_location=self.device, weights_only=True)
+        self.load_state_dict(ck["model"])
+        for key in ("_output_normalizer", "_node_normalizer", "_edge_normalizer"):
+            st, nrm = ck.get(key, {}), getattr(self, key, None)
+            if nrm is not None and st:
+                for k, v in st.items():
+                    setattr(nrm, k, v)
+
+    def save_checkpoint(self, savedir: Optional[str] = None) -> None:
+        savedir = savedir or self.model_dir
+        os.makedirs(os.path.dirname(savedir) or ".", exist_ok=True)
+        torch.save({
+            "model": self.state_dict(),
+            "_output_normalizer": self._output_normalizer.get_variable(),
+            "_node_normalizer": self._node_normalizer.get_variable(),
+            "_edge_normalizer": (self._edge_normalizer.get_variable() if self._edge_normalizer
+                                 else None),
+        }, savedir)

@@ -1,0 +1,61 @@
+"""Graph-sharded data parallelism: one process per GPU, each rank collates its own
+graphs (block-diagonal batches never share edges), one RCCL exchange per step.
+
+Exact equivalence with the single-process reference step on the union of all ranks' graphs needs
+three things the reference never had to do (it runs devices=1, reference train.py:233-236):
+  1. Normalizer batch statistics summed across ranks before they are accumulated
+     (Simulator.set_process_group → Normalizer._accumulate all-reduce);
+  2. the masked-mean loss divided by the GLOBAL masked-node count (global_masked_mse);
+  3. parameter gradients SUMMED across ranks — with (2) that is the gradient of the global loss.
+Gradients of EncodeProcessDecode live in one flat buffer, so (3) is a single all-reduce.
+"""
+import torch
+import torch.distributed as dist
+
+from graphphysics.utils.loss import _prepare_mask_for_loss
+
+
+def global_masked_mse(target, network_output, node_type, masks, group=None):
+    """L2Loss (reference utils/loss.py:28-65) over the union of all ranks' nodes: returns the local
+    contribution Σ_local err² / N_global, whose sum over ranks is the global masked mean."""
+    mask = _prepare_mask_for_loss(network_output, node_type, masks)
+    err = ((network_output - target) ** 2)[mask]
+    cnt = torch.tensor([float(err.numel())], device=err.device)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(cnt, group=group)
+    return err.sum() / cnt[0]
+
+
+def flat_grad_buffer(params):
+    """The single contiguous tensor all gradients are views of, or None."""
+    gs = [p.grad for p in params if p.grad is not None]
+    if not gs:
+        return None
+    st = gs[0].untyped_storage()
+    off = gs[0].storage_offset()
+    for g in gs:
+        if g.untyped_storage().data_ptr() != st.data_ptr() or g.storage_offset() != off \
+                or not g.is_contiguous():
+            return None
+        off += g.numel()
+    n = off - gs[0].storage_offset()
+    return torch.empty(0, dtype=gs[0].dtype, device=gs[0].device).set_(st, gs[0].storage_offset(), (n,))
+
+
+def allreduce_gradients(params, group=None, op=None):
+    """Sum gradients over ranks (one collective when they share a flat buffer)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    op = op if op is not None else dist.ReduceOp.SUM
+    params = list(params)
+    flat = flat_grad_buffer(params)
+    if flat is not None:
+        dist.all_reduce(flat, op=op, group=group)
+        return
+    gs = [p.grad for p in params if p.grad is not None]
+    buf = torch.cat([g.reshape(-1) for g in gs])
+    dist.all_reduce(buf, op=op, group=group)
+    o = 0
+    for g in gs:
+        g.copy_(buf[o:o + g.numel()].view_as(g))
+        o += g.numel()

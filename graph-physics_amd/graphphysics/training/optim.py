@@ -1,0 +1,88 @@
+"""Fused AdamW on MI355X: one mgn_adamw launch over the flat parameter buffer.
+
+Semantics of torch.optim.AdamW as the reference configures it (reference
+graphphysics/training/lightning_module.py:275-292: lr, weight_decay=1e-4, betas=(0.9, 0.95),
+eps=1e-8): decoupled decay p *= 1 - lr*wd, exp_avg lerp, exp_avg_sq, bias-corrected step.
+When the parameters and their gradients are consecutive views of one buffer each (what
+EncodeProcessDecode sets up), the whole model is updated by a single kernel; otherwise one launch
+per parameter. Parameters must live on a HIP device.
+"""
+import torch
+
+from graphphysics import _native as nat
+
+
+def _flat_span(tensors):
+    """If tensors are consecutive, contiguous views of one storage, return (base_tensor_view)."""
+    if not tensors:
+        return None
+    t0 = tensors[0]
+    st = t0.untyped_storage().data_ptr()
+    off = t0.storage_offset()
+    for t in tensors:
+        if (t.untyped_storage().data_ptr() != st or t.storage_offset() != off
+                or not t.is_contiguous() or t.dtype != torch.float32):
+            return None
+        off += t.numel()
+    n = off - t0.storage_offset()
+    return torch.empty(0, dtype=torch.float32, device=t0.device).set_(
+        t0.untyped_storage(), t0.storage_offset(), (n,))
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        L = nat.lib()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            for p in ps:
+                nat.require_device(p)
+            b1, b2 = group["betas"]
+            if "flat_state" not in group or group.get("flat_members") != [id(p) for p in ps]:
+                self._init_state(group, ps)
+            group["step_count"] = group.get("step_count", 0) + 1
+            step = group["step_count"]
+            st = nat.stream_ptr(ps[0].device)
+            fp, fg = _flat_span(ps), _flat_span([p.grad for p in ps])
+            fm, fv = group["flat_state"]
+            if fp is not None and fg is not None:
+                nat.check(L.mgn_adamw(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
+                                      group["lr"], b1, b2, group["eps"], group["weight_decay"], step, st))
+            else:
+                for p in ps:
+                    s = self.state[p]
+                    g = p.grad.contiguous()
+                    nat.check(L.mgn_adamw(nat.ptr(p), nat.ptr(g), nat.ptr(s["exp_avg"]),
+                                          nat.ptr(s["exp_avg_sq"]), p.numel(), group["lr"], b1, b2,
+                                          group["eps"], group["weight_decay"], step, st))
+            for p in ps:
+                self.state[p]["step"] = torch.tensor(float(step))
+        return loss
+
+    def _init_state(self, group, ps):
+        n = sum(p.numel() for p in ps)
+        dev = ps[0].device
+        fm = torch.zeros(n, dtype=torch.float32, device=dev)
+        fv = torch.zeros(n, dtype=torch.float32, device=dev)
+        o = 0
+        for p in ps:
+            k = p.numel()
+            s = self.state[p]
+            m_old, v_old = s.get("exp_avg"), s.get("exp_avg_sq")
+            if m_old is not None:
+                fm[o:o + k].copy_(m_old.reshape(-1))
+                fv[o:o + k].copy_(v_old.reshape(-1))
+            s["exp_avg"] = fm[o:o + k].view_as(p)
+            s["exp_avg_sq"] = fv[o:o + k].view_as(p)
+            o += k
+        group["flat_state"] = (fm, fv)
+        group["flat_members"] = [id(p) for p in ps]

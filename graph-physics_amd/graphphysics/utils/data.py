@@ -1,0 +1,20 @@
+"""Graph container. Uses torch_geometric.data.Data when installed (reference
+graphphysics/models/simulator.py:7); otherwise a minimal attribute bag with the fields the MGN
+path reads (x, edge_index, edge_attr, pos, y)."""
+try:  # pragma: no cover - PyG is not installed in this image
+    from torch_geometric.data import Data  # noqa: F401
+except ImportError:  # pragma: no cover
+    class Data:
+        def __init__(self, **kw):
+            for k, v in kw.items():
+                setattr(self, k, v)
+
+        @property
+        def num_nodes(self):
+            return self.x.size(0) if getattr(self, "x", None) is not None else None
+
+        def to(self, device):
+            for k, v in list(vars(self).items()):
+                if hasattr(v, "to"):
+                    setattr(self, k, v.to(device))
+            return self

@@ -1,0 +1,171 @@
+/*
+ * libmgn — MI355X-native (gfx950) MeshGraphNet message-passing library. C ABI.
+ *
+ * This is the drop-in boundary for the hot path of cviviers/graph-physics: everything the
+ * reference executes from EncodeProcessDecode.forward downwards (reference
+ * graphphysics/models/processors.py:111-137) and its autograd backward:
+ *
+ *   mgn_topology_build   replaces the index bookkeeping torch-geometric 2.6.1 does inside
+ *                        MessagePassing.propagate for edge_index[2,E] (reference
+ *                        graphphysics/models/layers.py:688-696: row,col = edge_index; x[col],
+ *                        x[row]; scatter-add over edge_index[1] with dim_size = x.size(0)).
+ *   mgn_mlp_pack         nn.Linear weights of build_mlp (layers.py:77-113) → MFMA fragment order.
+ *   mgn_mlp_forward      build_mlp forward (Linear/ReLU chain + RMSNorm layers.py:49-74);
+ *                        used for nodes_encoder / edges_encoder / decode_module
+ *                        (processors.py:72-90,127-128,136).
+ *   mgn_mlp_backward     its backward (data + weight gradients).
+ *   mgn_block_forward    GraphNetBlock.forward (layers.py:667-746): edge MLP on
+ *                        [e ‖ x[col] ‖ x[row]], sum-aggregation into targets, node MLP on
+ *                        [x ‖ aggr], both residuals.
+ *   mgn_block_backward   its backward (index_put_/gather/addmm backward of the reference).
+ *   mgn_adamw            torch.optim.AdamW step (lightning_module.py:275-282) over a flat
+ *                        parameter buffer.
+ *
+ * Conventions
+ *  - All device memory is owned by the caller (PyTorch caching allocator); raw pointers + sizes.
+ *    The library holds no device allocations and no global mutable state besides the
+ *    thread-local error string. Every call is asynchronous on the given stream except
+ *    mgn_topology_build (which reads back one validation word).
+ *  - Return value: 0 on success, otherwise a nonzero status; mgn_last_error() describes it.
+ *  - Edge order inside the library is target-sorted ("CSC" order: stable sort of the caller's
+ *    edges by edge_index[1]); csc_eid maps it back to the caller's order.
+ *  - dtype: MGN_F32 = fp32 storage + exact fp32 MFMA (parity path);
+ *           MGN_BF16 = bf16 storage of activations/packed weights, fp32 accumulation and fp32
+ *           epilogues (RMSNorm, residual), fp32 master weights and gradients.
+ *  - Deterministic: no floating-point atomics; every reduction has a fixed order.
+ */
+#ifndef MGN_H
+#define MGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
+
+#define MGN_ABI_VERSION 1
+#define MGN_F32 0
+#define MGN_BF16 1
+#define MGN_MAX_LAYERS 8
+
+/* ---------------------------------------------------------------- status */
+int mgn_abi_version(void);
+const char* mgn_last_error(void);
+
+/* ---------------------------------------------------------------- topology */
+typedef struct mgn_topology {
+    int64_t num_nodes;
+    int64_t num_edges;
+    const int32_t* csc_src;  /* [E] source node (edge_index[0]) of the k-th target-sorted edge  */
+    const int32_t* csc_dst;  /* [E] target node (edge_index[1]), non-decreasing                  */
+    const int32_t* csc_eid;  /* [E] caller edge id of the k-th target-sorted edge                */
+    const int32_t* col_ptr;  /* [N+1] in-edge segment of node i = [col_ptr[i], col_ptr[i+1])     */
+    const int32_t* row_ptr;  /* [N+1] out-edge segment of node j within row_perm                 */
+    const int32_t* row_perm; /* [E] target-sorted positions, stably sorted by source node         */
+} mgn_topology;
+
+size_t mgn_topology_workspace_bytes(int64_t num_edges, int64_t num_nodes);
+/* edge_index: device int64 [2,E] row-major (reference layout). Fails with a nonzero status and
+ * "edge_index out of range" if any index is outside [0, N) (the reference raises IndexError). */
+int mgn_topology_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                       int32_t* csc_src, int32_t* csc_dst, int32_t* csc_eid, int32_t* col_ptr,
+                       int32_t* row_ptr, int32_t* row_perm, void* ws, size_t ws_bytes,
+                       mgn_stream_t stream);
+
+/* ---------------------------------------------------------------- MLP (build_mlp) */
+typedef struct mgn_mlp {
+    int32_t n_layers; /* number of nn.Linear (reference nb_of_layers, >= 2)                    */
+    int32_t in_dim;   /* input features of Linear 0                                          */
+    int32_t hidden;   /* hidden width (16, 32, 64 or 128)                                    */
+    int32_t out_dim;  /* output features of the last Linear (== hidden, or 1..16)            */
+    int32_t has_norm; /* RMSNorm(out_dim) after the last Linear                              */
+    int32_t dtype;    /* MGN_F32 | MGN_BF16                                                  */
+    const void* wpack;  /* forward fragments, mgn_mlp_pack_elems() elements of dtype         */
+    const void* wtpack; /* transposed fragments (backward), same element count                */
+    const float* bias[MGN_MAX_LAYERS]; /* fp32 master biases                                  */
+    const float* scale;                /* fp32 RMSNorm scale [out_dim] or NULL                */
+} mgn_mlp;
+
+typedef struct mgn_mlp_saved {
+    void* act;    /* [(n_layers-1), M, hidden] post-ReLU activations (dtype)                  */
+    void* z;      /* [M, out_dim] last Linear output before RMSNorm (dtype); unused w/o norm  */
+    float* rden;  /* [M] RMSNorm denominator rms+eps                                          */
+} mgn_mlp_saved;
+
+/* Pack job: one nn.Linear weight [n, k] fp32 row-major → fragment buffers (dtype). */
+typedef struct mgn_pack_job {
+    const float* w;
+    void* dst;   /* forward fragments  */
+    void* dstT;  /* transposed fragments */
+    int32_t n, k, dtype, reserved;
+} mgn_pack_job;
+
+int64_t mgn_linear_pack_elems(int32_t n, int32_t k, int32_t dtype);
+int64_t mgn_mlp_pack_elems(const mgn_mlp* m); /* Σ over layers of mgn_linear_pack_elems */
+/* jobs: DEVICE array of njobs mgn_pack_job; max_elems = max over jobs of n*k. One launch. */
+int mgn_pack_weights(const mgn_pack_job* jobs, int32_t njobs, int64_t max_elems,
+                     mgn_stream_t stream);
+
+/* Input description of a dense MLP: rows r of `in` (ld elements apart), optionally gathered
+ * through in_rows[r]; in_dtype MGN_F32 or the MLP dtype. */
+int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                    const int32_t* in_rows, int64_t rows, void* out, int32_t out_dtype,
+                    mgn_mlp_saved* saved, mgn_stream_t stream);
+size_t mgn_mlp_backward_workspace_bytes(const mgn_mlp* m, int64_t rows);
+/* grads: flat fp32 [W0, b0, W1, b1, ..., W_{L-1}, b_{L-1}, scale] (nn.Module parameter order),
+ * overwritten. din (optional, NULL to skip): gradient w.r.t. the (gathered) input rows. */
+int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                     const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved,
+                     const void* dout, int32_t dout_dtype, void* din, int32_t din_dtype,
+                     float* grads, void* ws, size_t ws_bytes, mgn_stream_t stream);
+
+/* ---------------------------------------------------------------- GraphNetBlock */
+typedef struct mgn_block_saved {
+    mgn_mlp_saved edge; /* rows = E (target-sorted order) */
+    mgn_mlp_saved node; /* rows = N */
+    void* aggr;         /* [N, hidden] aggregated messages (dtype) */
+} mgn_block_saved;
+
+/* x:[N,h], e:[E,h] (target-sorted edge order), dtype of the MLPs. x_out/e_out may not alias. */
+int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                      const void* x, const void* e, void* x_out, void* e_out,
+                      mgn_block_saved* saved, mgn_stream_t stream);
+size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
+                                          const mgn_mlp* node);
+/* dx/de: gradients w.r.t. the block inputs (overwritten). edge_grads/node_grads: flat fp32 as
+ * in mgn_mlp_backward (overwritten). */
+int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                       const void* x, const void* e, const mgn_block_saved* saved,
+                       const void* dx_out, const void* de_out, void* dx, void* de,
+                       float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                       mgn_stream_t stream);
+
+/* ---------------------------------------------------------------- primitives */
+/* out[k,:] = in[idx[k],:] (gather), or out[idx[k],:] = in[k,:] when scatter != 0. */
+int mgn_permute_rows(const void* in, void* out, const int32_t* idx, int64_t rows, int32_t cols,
+                     int32_t in_dtype, int32_t out_dtype, int32_t scatter, mgn_stream_t stream);
+/* Segment sum over target-sorted edges: out[i,:] = Σ_{k in [col_ptr[i], col_ptr[i+1])} src[k,:].
+ * The stand-alone form of the aggregation fused into mgn_block_forward. */
+int mgn_segment_sum(const void* src, const int32_t* seg_ptr, int64_t segments, int32_t cols,
+                    int32_t dtype, void* out, mgn_stream_t stream);
+
+/* torch.optim.AdamW semantics (decoupled weight decay p *= 1 - lr*wd, bias-corrected moments,
+ * denominator sqrt(v)/sqrt(1-beta2^t) + eps), fp32, over n contiguous elements. */
+int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+              double lr, double beta1, double beta2, double eps, double weight_decay,
+              int64_t step, mgn_stream_t stream);
+
+/* ---------------------------------------------------------------- opt-in profiler */
+/* Kernel classes: 0 edge-MLP fwd, 1 node-MLP fwd, 2 dense-MLP fwd, 3 edge-MLP bwd-data,
+ * 4 node-MLP bwd-data, 5 dense-MLP bwd-data, 6 weight-grad, 7 weight-grad reduce,
+ * 8 node-gradient combine, 9 weight pack, 10 AdamW. */
+int mgn_profile_enable(int on);
+int mgn_profile_collect(int kind, double* total_ms, int64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGN_H */

@@ -1,0 +1,287 @@
+"""GPU parity: libmgn (HIP, gfx950) vs the oracle / the reference's golden vectors.
+
+Tolerances (stated per test):
+  fp32 forward        max|Δ| ≤ 1e-5·(1+|ref|) elementwise vs the CPU fp32 oracle (= reference ops)
+  fp32 gradients      rel-L2 vs the fp64 evaluation of the same algorithm ≤
+                      max(1e-5, 2 × the reference CPU-fp32 path's own rel-L2 error vs fp64).
+                      (Measured: the reference's fp32 CPU path is 1e-3 off fp64 on dx at h=128 —
+                      a ReLU mask flip — while libmgn fp32 is 3e-7 off; comparing two fp32 paths
+                      directly would test the reference's rounding luck, not parity.)
+  bf16 (perf path)    rel-L2 ≤ 1e-2 forward, ≤ 1.5e-1 gradients vs fp64 (bf16 activations move
+                      ReLU masks by design; training-level accuracy is checked by one-step MSE).
+  integer / index work (topology, permutations) bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    import __graft_entry__ as ge
+
+    ge.build()
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+def _load(name):
+    z = np.load(os.path.join(G, name))
+    return {k: z[k] for k in z.files}
+
+
+def relerr(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def assert_grad_close(got, ref, tol=1e-3, outlier_frac=3e-3):
+    """SURVEY §8c grads bound rel-L2 ≤ tol. fp32 sums in another order can move a pre-activation
+    that is within rounding of 0 across the ReLU boundary; that flips one mask element and changes
+    the gradient of the (few) rows touching it. So: overall rel-L2 ≤ 2·tol, and after dropping the
+    worst `outlier_frac` of rows, rel-L2 ≤ tol/10."""
+    got, ref = got.detach().double().cpu(), ref.detach().double().cpu()
+    assert relerr(got, ref) <= 2 * tol, relerr(got, ref)
+    if got.dim() == 2 and got.shape[0] >= 100:
+        rowerr = (got - ref).norm(dim=1)
+        keep = rowerr.argsort()[: got.shape[0] - int(np.ceil(outlier_frac * got.shape[0]))]
+        assert relerr(got[keep], ref[keep]) <= tol / 10, relerr(got[keep], ref[keep])
+
+
+def assert_vs_truth(got, ref32, ref64, floor=1e-5):
+    """fp32 parity: no further from the fp64 truth than the reference's own fp32 path (x2)."""
+    e_ref = relerr(ref32, ref64)
+    e_got = relerr(got, ref64)
+    assert e_got <= max(floor, 2 * e_ref), f"libmgn {e_got:.2e} vs fp64, reference fp32 {e_ref:.2e}"
+
+
+def assert_close_elem(got, ref, tol=1e-5):
+    got, ref = got.detach().double().cpu(), ref.detach().double().cpu()
+    bad = (got - ref).abs() > tol * (1 + ref.abs())
+    assert not bad.any(), f"max err {(got - ref).abs().max().item()} at {bad.nonzero()[:4].tolist()}"
+
+
+# ----------------------------------------------------------------------------- topology
+def test_topology_matches_stable_sort():
+    from graphphysics.models import _engine
+
+    g = torch.Generator().manual_seed(3)
+    n, e = 97, 1000
+    ei = torch.randint(0, n, (2, e), generator=g)
+    t = _engine.GraphTopology(ei.to(DEV), n)
+    col, row = ei[1].numpy(), ei[0].numpy()
+    perm = np.argsort(col, kind="stable")
+    assert np.array_equal(t.csc_eid.cpu().numpy(), perm)
+    assert np.array_equal(t.csc_dst.cpu().numpy(), col[perm])
+    assert np.array_equal(t.csc_src.cpu().numpy(), row[perm])
+    assert np.array_equal(t.col_ptr.cpu().numpy(), np.searchsorted(col[perm], np.arange(n + 1)))
+    rp = np.argsort(row[perm], kind="stable")
+    assert np.array_equal(t.row_perm.cpu().numpy(), rp)
+    assert np.array_equal(t.row_ptr.cpu().numpy(), np.searchsorted(row[perm][rp], np.arange(n + 1)))
+
+
+def test_topology_rejects_out_of_range():
+    from graphphysics.models import _engine
+
+    with pytest.raises(IndexError):
+        _engine.GraphTopology(torch.tensor([[0, 1], [1, 5]], device=DEV), 4)
+
+
+# ----------------------------------------------------------------------------- block
+def _block_from_golden(z, dtype):
+    from graphphysics.models.layers import GraphNetBlock
+
+    blk = GraphNetBlock(16)
+    blk.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w::")})
+    blk.compute_dtype = dtype
+    return blk.to(DEV)
+
+
+def test_block_cycle_vs_golden_fp32():
+    z = _load("block_cycle_h16.npz")
+    blk = _block_from_golden(z, torch.float32)
+    x = torch.from_numpy(z["x"]).to(DEV).requires_grad_(True)
+    e = torch.from_numpy(z["e"]).to(DEV).requires_grad_(True)
+    ei = torch.from_numpy(z["edge_index"]).to(DEV)
+    x2, e2 = blk(x, ei, e)
+    ((x2 * torch.from_numpy(z["gx"]).to(DEV)).sum() + (e2 * torch.from_numpy(z["ge"]).to(DEV)).sum()).backward()
+    assert_close_elem(x2, torch.from_numpy(z["x_out"]))
+    assert_close_elem(e2, torch.from_numpy(z["e_out"]))
+    assert relerr(x.grad, torch.from_numpy(z["x_grad"])) < 1e-4
+    assert relerr(e.grad, torch.from_numpy(z["e_grad"])) < 1e-4
+    for k, p in blk.named_parameters():
+        assert relerr(p.grad, torch.from_numpy(z["g::" + k])) < 1e-4, k
+
+
+def _cyl_graph():
+    from graphphysics.utils import meshes
+
+    m = meshes.load_cylinder_mesh()
+    n = m["pos"].shape[0]
+    ei = meshes.triangles_to_edge_index(m["triangles"], n)
+    return n, torch.from_numpy(ei)
+
+
+@pytest.mark.parametrize("dtype,tf,tg", [(torch.float32, 1e-5, None), (torch.bfloat16, 1e-2, 1.5e-1)])
+def test_block_cylinder_h128_vs_oracle(dtype, tf, tg):
+    from graphphysics.models.layers import GraphNetBlock
+
+    n, ei = _cyl_graph()
+    h = 128
+    torch.manual_seed(0)
+    blk = GraphNetBlock(h)
+    ref_p = {k: v.detach().clone().requires_grad_(True) for k, v in blk.named_parameters()}
+    g = torch.Generator().manual_seed(1234)
+    x = torch.randn(n, h, generator=g)
+    e = torch.randn(ei.shape[1], h, generator=g)
+    gx = torch.randn(n, h, generator=g)
+    ge = torch.randn(ei.shape[1], h, generator=g)
+    xr, er = x.clone().requires_grad_(True), e.clone().requires_grad_(True)
+    x2r, e2r = O.graph_net_block(xr, ei, er, ref_p)
+    ((x2r * gx).sum() + (e2r * ge).sum()).backward()
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in ref_p.items()}
+    x64, e64 = x.double().requires_grad_(True), e.double().requires_grad_(True)
+    x2d, e2d = O.graph_net_block(x64, ei, e64, p64)
+    ((x2d * gx.double()).sum() + (e2d * ge.double()).sum()).backward()
+
+    blk.compute_dtype = dtype
+    blk = blk.to(DEV)
+    xd, ed = x.to(DEV).requires_grad_(True), e.to(DEV).requires_grad_(True)
+    x2, e2 = blk(xd, ei.to(DEV), ed)
+    ((x2 * gx.to(DEV)).sum() + (e2 * ge.to(DEV)).sum()).backward()
+    if dtype == torch.float32:
+        assert_close_elem(x2, x2r, tf)
+        assert_close_elem(e2, e2r, tf)
+        assert_vs_truth(xd.grad, xr.grad, x64.grad)
+        assert_vs_truth(ed.grad, er.grad, e64.grad)
+        for k, p in blk.named_parameters():
+            assert_vs_truth(p.grad, ref_p[k].grad, p64[k].grad)
+    else:
+        assert relerr(x2, x2d) < tf and relerr(e2, e2d) < tf
+        assert relerr(xd.grad, x64.grad) < tg and relerr(ed.grad, e64.grad) < tg
+        for k, p in blk.named_parameters():
+            assert relerr(p.grad, p64[k].grad) < tg, k
+
+
+# ----------------------------------------------------------------------------- full model
+def test_epd_random_multigraph_vs_golden():
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    z = _load("epd_random_h16.npz")
+    m = EncodeProcessDecode(3, 8, 4, 3, 16, compute_dtype=torch.float32)
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w::")})
+    m = m.to(DEV)
+    y = m(Data(x=torch.from_numpy(z["x"]).to(DEV), edge_index=torch.from_numpy(z["edge_index"]).to(DEV),
+               edge_attr=torch.from_numpy(z["edge_attr"]).to(DEV)))
+    (y * torch.from_numpy(z["gy"]).to(DEV)).sum().backward()
+    assert_close_elem(y, torch.from_numpy(z["y"]))
+    for k, p in m.named_parameters():
+        assert relerr(p.grad, torch.from_numpy(z["g::" + k])) < 1e-4, k
+    # only_processor on the same multigraph (duplicates + self loops)
+    p = EncodeProcessDecode(3, 16, 16, 3, 16, only_processor=True, compute_dtype=torch.float32)
+    p.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("opw::")})
+    p = p.to(DEV)
+    xl = torch.from_numpy(z["op_x"]).to(DEV).requires_grad_(True)
+    el = torch.from_numpy(z["op_e"]).to(DEV).requires_grad_(True)
+    yl = p(Data(x=xl, edge_index=torch.from_numpy(z["edge_index"]).to(DEV), edge_attr=el))
+    (yl * torch.from_numpy(z["op_g"]).to(DEV)).sum().backward()
+    assert_close_elem(yl, torch.from_numpy(z["op_y"]))
+    assert relerr(xl.grad, torch.from_numpy(z["op_x_grad"])) < 1e-4
+    assert relerr(el.grad, torch.from_numpy(z["op_e_grad"])) < 1e-4
+
+
+@pytest.mark.parametrize("mp,h,dtype,tf,tg", [(5, 32, torch.float32, 1e-4, None),
+                                              (15, 128, torch.float32, 1e-4, None),
+                                              (15, 128, torch.bfloat16, 3e-2, 1.5e-1)])
+def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    n, ei = _cyl_graph()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(ei.shape[1], 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    rp = dict(ref.named_parameters())
+    yr = O.encode_process_decode(x, ei, ea, rp, mp)
+    (yr * gy).sum().backward()
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(x.double(), ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=dtype).to(DEV)
+    y = m(Data(x=x.to(DEV), edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+    (y * gy.to(DEV)).sum().backward()
+    assert relerr(y, yr) < tf
+    for k, p in m.named_parameters():
+        if tg is None:
+            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad)
+        else:
+            assert relerr(p.grad, p64[k].grad) < tg, k
+
+
+# ----------------------------------------------------------------------------- optimiser / primitives
+def test_adamw_matches_torch():
+    from graphphysics.training.optim import FusedAdamW
+
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(1000, generator=g)
+    ref = torch.nn.Parameter(w.clone())
+    mine = torch.nn.Parameter(w.clone().to(DEV))
+    o1 = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
+    o2 = FusedAdamW([mine], lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
+    for _ in range(5):
+        gr = torch.randn(1000, generator=g)
+        ref.grad = gr.clone()
+        mine.grad = gr.to(DEV)
+        o1.step()
+        o2.step()
+    torch.testing.assert_close(mine.detach().cpu(), ref.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_segment_sum_and_permute():
+    from graphphysics import _native as nat
+
+    L = nat.lib()
+    g = torch.Generator().manual_seed(1)
+    rows, cols, segs = 500, 24, 60
+    src = torch.randn(rows, cols, generator=g)
+    cuts = torch.sort(torch.randint(0, rows + 1, (segs - 1,), generator=g)).values
+    ptr = torch.cat([torch.tensor([0]), cuts, torch.tensor([rows])]).int()
+    out = torch.empty(segs, cols, device=DEV)
+    nat.check(L.mgn_segment_sum(nat.ptr(src.to(DEV)), nat.ptr(ptr.to(DEV)), segs, cols, nat.MGN_F32,
+                                nat.ptr(out), nat.stream_ptr()))
+    ref = torch.stack([src[ptr[i]:ptr[i + 1]].sum(0) for i in range(segs)])
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-5)
+    idx = torch.randperm(rows, generator=g).int()
+    srcd = src.to(DEV)
+    gath = torch.empty(rows, cols, device=DEV)
+    nat.check(L.mgn_permute_rows(nat.ptr(srcd), nat.ptr(gath), nat.ptr(idx.to(DEV)), rows, cols, nat.MGN_F32,
+                                 nat.MGN_F32, 0, nat.stream_ptr()))
+    assert torch.equal(gath.cpu(), src[idx.long()])
+
+
+def test_empty_edge_set():
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(2, 5, 3, 2, 16, compute_dtype=torch.float32).to(DEV)
+    x = torch.randn(6, 5)
+    y = m(Data(x=x.to(DEV), edge_index=torch.zeros((2, 0), dtype=torch.long, device=DEV),
+               edge_attr=torch.zeros((0, 3), device=DEV)))
+    torch.manual_seed(0)
+    ref = O.OracleEPD(2, 5, 3, 2, 16)
+    yr = O.encode_process_decode(x, torch.zeros((2, 0), dtype=torch.long), torch.zeros((0, 3)),
+                                 dict(ref.named_parameters()), 2)
+    assert relerr(y, yr) < 1e-4
