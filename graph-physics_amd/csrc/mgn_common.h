@@ -163,3 +163,29 @@ struct ProfScope {
     ProfScope(int kind, hipStream_t s) : slot(mgn_prof_begin(kind, s)), st(s) {}
     ~ProfScope() { mgn_prof_end(slot, st); }
 };
+
+// --------------------------------------------------------------------------- saved-activation layout
+// Row-octet ("R8") layout of a [rows x cols] matrix: element (m, c) at ((m/8)*cols + c)*8 + m%8.
+// Eight consecutive rows of one column are contiguous (16 B in bf16): exactly one MFMA operand
+// fragment when the reduction runs over rows (weight gradients), so the weight-gradient GEMMs load
+// operands straight from HBM/L2 with 16-byte loads and no LDS transposition.
+__host__ __device__ __forceinline__ int64_t r8_index(int64_t m, int64_t c, int64_t cols) {
+    return ((m >> 3) * cols + c) * 8 + (m & 7);
+}
+// Saved buffers cover rows padded to 64 (every tile, including pure-padding rows, is written).
+__host__ __device__ __forceinline__ int64_t rows_pad(int64_t M) { return (M + 63) / 64 * 64; }
+__host__ __device__ __forceinline__ int kstep_of(int dtype) { return dtype == MGN_BF16 ? 32 : 4; }
+// R8 column count of the saved INPUT of layer l (layer 0: padded MLP input; else padded hidden)
+__host__ __device__ inline int act_cols(const mgn_mlp& m, int l) {
+    const int ks = kstep_of(m.dtype);
+    return l == 0 ? rup(m.in_dim, ks) : rup(m.hidden, ks);
+}
+__host__ __device__ inline int64_t act_off(const mgn_mlp& m, int64_t M, int l) {
+    int64_t o = 0;
+    for (int j = 0; j < l; ++j) o += rows_pad(M) * act_cols(m, j);
+    return o;
+}
+// ReLU masks of the hidden-layer outputs: per layer, per (16-row tile, 16-col tile), 4 ballot words
+__host__ __device__ inline int64_t mask_words_per_layer(const mgn_mlp& m, int64_t M) {
+    return rows_pad(M) / 16 * (m.hidden / 16) * 4;
+}

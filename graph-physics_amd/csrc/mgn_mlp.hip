@@ -125,6 +125,27 @@ __device__ void load_tile(T* In, int ldi, int K0, int KP, const SrcSeg* seg, int
         }
 }
 
+// Write an LDS tile (BM rows x cols, row-major, leading dim ldl) to an R8 matrix with `cols`
+// columns, rows [row0, row0 + BM). One item = one (row octet, column) = 8 LDS reads, one 16/32-B store.
+template <class T, int BM>
+__device__ void copy_out_r8(const T* lds, int ldl, int cols, T* dst, int64_t row0) {
+    constexpr int OCT = BM / 8;
+    const int64_t o0 = row0 >> 3;
+    for (int it = threadIdx.x; it < OCT * cols; it += MGN_THREADS) {
+        const int o = it / cols, c = it - o * cols;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = to_f(lds[(size_t)(o * 8 + q) * ldl + c]);
+        T* p = dst + ((o0 + o) * cols + c) * 8;
+        if (sizeof(T) == 2) {
+            Chunk<T>::store(p, v);
+        } else {
+            Chunk<T>::store(p, v);
+            Chunk<T>::store(p + 4, v + 4);
+        }
+    }
+}
+
 // --------------------------------------------------------------------------- forward
 struct FwdArgs {
     SrcSeg seg[3];
@@ -146,7 +167,10 @@ struct FwdArgs {
     int32_t out_dtype;
     int64_t out_ld;
     const void* resid;
-    void* act_save;
+    void* act8;                          // R8 saved layer inputs
+    int64_t act_off[MGN_MAX_LAYERS];     // element offset of layer l's R8 block
+    unsigned long long* mask;            // ReLU ballot words of hidden layers
+    int64_t mask_stride;                 // words per hidden layer
     void* z_save;
     float* rden_save;
 };
@@ -276,6 +300,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
         }
     }
     __syncthreads();
+    copy_out_r8<T, BM>(In, a.ldi, KP0, reinterpret_cast<T*>(a.act8) + a.act_off[0], row0);
 
     const T* wp = reinterpret_cast<const T*>(a.wpack);
     const T* cur = In;
@@ -297,8 +322,13 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = fmaxf(g.acc[i][j][r] + bb[r], 0.f);
                     st4(nxt + (size_t)m * a.ldh + n, v);
-                    const int64_t row = row0 + m;
-                    if (row < a.M) st4(reinterpret_cast<T*>(a.act_save) + ((int64_t)l * a.M + row) * H + n, v);
+                    const int64_t mtile = (row0 >> 4) + g.mt0 + j;
+                    unsigned long long* mw = a.mask + (int64_t)l * a.mask_stride + (mtile * NTH + g.nt0 + i) * 4;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const unsigned long long bits = __ballot(v[r] > 0.f);
+                        if ((threadIdx.x & 63) == 0) mw[r] = bits;
+                    }
                 }
             }
         }
@@ -308,6 +338,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
                 nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
         }
         __syncthreads();
+        copy_out_r8<T, BM>(nxt, a.ldh, rup(H, KSTEP), reinterpret_cast<T*>(a.act8) + a.act_off[l + 1], row0);
         wp += linear_pack_elems(H, K, dtype_id<T>());
         cur = nxt;
         ldc = a.ldh;
@@ -332,7 +363,8 @@ struct BwdArgs {
     float dinv;
     const void* wtpack;
     const float* scale;
-    const void* act_save;
+    const unsigned long long* mask;  // ReLU ballot words (forward)
+    int64_t mask_stride;
     const void* z_save;
     const float* rden_save;
     const void* dout;
@@ -340,7 +372,8 @@ struct BwdArgs {
     int64_t dout_ld;
     const void* gath;       // EDGE: d_aggr [N][H] (T), added at gath_idx[row]
     const int32_t* gath_idx;
-    void* dz_save;          // [L][M][H] (T)
+    void* dz8;              // [L] R8 blocks of [RP x H] (T): dZ of every layer, for the weight grads
+    int64_t RP;
     float* dscale_part;     // [gridDim.x][NOUT]
     void* din;              // DENSE: [M][din_ld] (din_dtype), optional
     int32_t din_dtype;
@@ -410,14 +443,11 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
                     dsc[v] += dy[v] * (z[v] / q);
                 }
             }
-            if (r < BM) {
-                st4(D0 + (size_t)r * a.ldh + cc, dz);
-                if (valid) st4(reinterpret_cast<T*>(a.dz_save) + ((int64_t)(a.L - 1) * a.M + row) * H + cc, dz);
-            }
+            if (r < BM) st4(D0 + (size_t)r * a.ldh + cc, dz);
         }
-        // zero pad columns [NO4, KPN) of D0
+        // zero pad columns [NO4, max(KPN, H)) of D0
         const int NO4 = CPR * 4;
-        const int padc = KPN - NO4;
+        const int padc = (KPN > H ? KPN : H) - NO4;
         if (padc > 0)
             for (int it = tid; it < BM * padc; it += MGN_THREADS) {
                 const int r = it / padc, c = it - r * padc;
@@ -439,6 +469,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         }
     }
     __syncthreads();
+    copy_out_r8<T, BM>(D0, a.ldh, H, reinterpret_cast<T*>(a.dz8) + (int64_t)(a.L - 1) * a.RP * H, row0);
 
     // ---- layers L-1 .. 1 : dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]
     const T* wt = reinterpret_cast<const T*>(a.wtpack);
@@ -458,6 +489,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         Gemm<T, NTH, MT> g;
         g.run(wt + off[l], cdiv(Nl, KSTEP), cur, a.ldh);
         if (g.active) {
+            const int lane = tid & 63;
 #pragma unroll
             for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i) {
                 const int k = g.n_of(i);
@@ -465,15 +497,12 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
                 for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
                     const int m = g.m_of(j);
                     const int64_t row = row0 + m;
+                    const int64_t mtile = (row0 >> 4) + g.mt0 + j;
+                    const unsigned long long* mw =
+                        a.mask + (int64_t)(l - 1) * a.mask_stride + (mtile * NTH + g.nt0 + i) * 4;
                     f4 v = g.acc[i][j];
-                    if (row < a.M) {
-                        const f4 act = ld4(reinterpret_cast<const T*>(a.act_save) + ((int64_t)(l - 1) * a.M + row) * H + k);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = act[r] > 0.f ? v[r] : 0.f;
-                        st4(reinterpret_cast<T*>(a.dz_save) + ((int64_t)(l - 1) * a.M + row) * H + k, v);
-                    } else {
-                        v = f4{0.f, 0.f, 0.f, 0.f};
-                    }
+                    for (int r = 0; r < 4; ++r) v[r] = ((mw[r] >> lane) & 1ull) && row < a.M ? v[r] : 0.f;
                     st4(nxt + (size_t)m * a.ldh + k, v);
                 }
             }
@@ -487,6 +516,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         T* t = cur;
         cur = nxt;
         nxt = t;
+        copy_out_r8<T, BM>(cur, a.ldh, H, reinterpret_cast<T*>(a.dz8) + (int64_t)(l - 1) * a.RP * H, row0);
     }
 
     // ---- layer 0 : dA0 = dZ_0 · W_0, K0 columns in chunks of H
@@ -529,169 +559,140 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 }
 
 // --------------------------------------------------------------------------- weight gradients
+// dW_l[n][k] = Σ_m dZ_l[m][n] · X_l[m][k], db_l[n] = Σ_m dZ_l[m][n]  (X_l = input of layer l).
+// Both operands are R8 matrices written by the forward/backward kernels, so each MFMA fragment
+// (VEC consecutive rows of one column) is a single 16-byte global load. A workgroup owns one
+// (layer, 128-column block) output tile over a chunk of rows; partial tiles go to fp32 slabs that
+// wgrad_reduce sums in a fixed order (deterministic, no atomics).
 struct WgJob {
-    int32_t layer, kb, n, k;
-    int64_t w_off, b_off;  // offsets in the flat grad vector; b_off < 0: no bias for this job
+    int32_t layer, kb, n, k, kp, pad;
+    int64_t w_off, b_off, act_off;  // b_off < 0: no bias for this job
 };
 struct WgArgs {
-    int64_t M;
-    int32_t rows_per_chunk, H, njobs, nseg;
-    const void* dz_save;
-    const void* act_save;
-    SrcSeg seg[3];
+    int64_t RP;
+    int32_t rows_per_chunk, H, njobs, pad;
+    const void* dz8;
+    const void* act8;
     WgJob job[12];
     float* part;
     int64_t G;
 };
 
-// Transposed staging of SR rows: dst[col][m] for col in [0, H), m in [0, SR).
-template <class T, int H, int SR>
-__device__ void stage_T_from(T* dst, int ldt, const T* src, int64_t src_ld, int ncols, int64_t r0,
-                             int64_t r1) {
-    constexpr int RG = 16 / sizeof(T);  // rows per 16-byte LDS write
-    constexpr int ITEMS = (H / 2) * (SR / RG);
-    for (int it = threadIdx.x; it < ITEMS; it += MGN_THREADS) {
-        const int cp = it % (H / 2), rg = it / (H / 2);
-        const int c = cp * 2, m0 = rg * RG;
-        float v0[RG], v1[RG];
-#pragma unroll
-        for (int q = 0; q < RG; ++q) {
-            const int64_t row = r0 + m0 + q;
-            v0[q] = 0.f;
-            v1[q] = 0.f;
-            if (row < r1 && c < ncols) {
-                const T* p = src + row * src_ld + c;
-                v0[q] = to_f(p[0]);
-                if (c + 1 < ncols) v1[q] = to_f(p[1]);
-            }
-        }
-        Chunk<T>::store(dst + (size_t)c * ldt + m0, v0);
-        Chunk<T>::store(dst + (size_t)(c + 1) * ldt + m0, v1);
-    }
-}
-
-template <class T, int H, int SR>
-__device__ void stage_T_segs(T* dst, int ldt, const SrcSeg* seg, int nseg, int kcol0, int K,
-                             int64_t r0, int64_t r1) {
-    constexpr int RG = 16 / sizeof(T);
-    constexpr int ITEMS = (H / 2) * (SR / RG);
-    for (int it = threadIdx.x; it < ITEMS; it += MGN_THREADS) {
-        const int cp = it % (H / 2), rg = it / (H / 2);
-        const int c = cp * 2, m0 = rg * RG;
-        float v0[RG], v1[RG];
-#pragma unroll
-        for (int q = 0; q < RG; ++q) {
-            v0[q] = 0.f;
-            v1[q] = 0.f;
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int kc = kcol0 + c + h;
-            if (kc >= K) continue;
-            int s = 0;
-            while (s + 1 < nseg && kc >= seg[s + 1].coff) ++s;
-            const SrcSeg& g = seg[s];
-            const int cl = kc - g.coff;
-#pragma unroll
-            for (int q = 0; q < RG; ++q) {
-                const int64_t row = r0 + m0 + q;
-                if (row < r1) {
-                    const float v = seg_load(g, row, cl);
-                    if (h == 0) v0[q] = v; else v1[q] = v;
-                }
-            }
-        }
-        Chunk<T>::store(dst + (size_t)c * ldt + m0, v0);
-        Chunk<T>::store(dst + (size_t)(c + 1) * ldt + m0, v1);
-    }
-}
-
 template <class T, int H>
 __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
-    constexpr int SR = 64;
-    constexpr int LDT = SR + 16 / sizeof(T);
     constexpr int NT = H / 16;
     using C = TileCfg<NT, NT>;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* ZT = reinterpret_cast<T*>(smem);
-    T* AT = ZT + H * LDT;
     const WgJob job = a.job[blockIdx.y];
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
-    const int64_t r_end = r_begin + a.rows_per_chunk < a.M ? r_begin + a.rows_per_chunk : a.M;
+    const int64_t r_end = r_begin + a.rows_per_chunk < a.RP ? r_begin + a.rows_per_chunk : a.RP;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
-    const bool active = mt0 < NT;
+    if (mt0 >= NT) return;
+    const T* Z = reinterpret_cast<const T*>(a.dz8) + (int64_t)job.layer * a.RP * H;
+    const T* X = reinterpret_cast<const T*>(a.act8) + job.act_off;
+    const int col0 = job.kb * H;
+    bool kon[C::MTW];
+#pragma unroll
+    for (int j = 0; j < C::MTW; ++j) kon[j] = col0 + (mt0 + j) * 16 < job.kp;
     f4 acc[C::NTW][C::MTW];
 #pragma unroll
     for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
         for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    float bacc = 0.f;
-    const T* dz = reinterpret_cast<const T*>(a.dz_save) + (int64_t)job.layer * a.M * H;
-    for (int64_t r0 = r_begin; r0 < r_end; r0 += SR) {
-        stage_T_from<T, H, SR>(ZT, LDT, dz, H, job.n, r0, r_end);
-        if (job.layer == 0)
-            stage_T_segs<T, H, SR>(AT, LDT, a.seg, a.nseg, job.kb * H, job.k, r0, r_end);
-        else
-            stage_T_from<T, H, SR>(AT, LDT,
-                                   reinterpret_cast<const T*>(a.act_save) + (int64_t)(job.layer - 1) * a.M * H,
-                                   H, H, r0, r_end);
-        __syncthreads();
-        if (active) {
+    float bsum[C::NTW];
 #pragma unroll
-            for (int ks = 0; ks < SR / KSTEP; ++ks) {
-                typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
+    for (int i = 0; i < C::NTW; ++i) bsum[i] = 0.f;
+    const bool do_bias = job.b_off >= 0 && wm == 0;
+    const typename Mf<T>::frag zero{};
+#pragma unroll 2
+    for (int64_t m0 = r_begin; m0 < r_end; m0 += KSTEP) {
+        const int64_t mr = m0 + VEC * (lane >> 4);
+        typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
 #pragma unroll
-                for (int i = 0; i < C::NTW; ++i)
-                    fa[i] = ld_frag(ZT + (size_t)((nt0 + i) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+        for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
 #pragma unroll
-                for (int j = 0; j < C::MTW; ++j)
-                    fb[j] = ld_frag(AT + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
-#pragma unroll
-                for (int i = 0; i < C::NTW; ++i)
-#pragma unroll
-                    for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
-            }
-        }
-        if (job.b_off >= 0 && threadIdx.x < H) {
-            const T* zr = ZT + (size_t)threadIdx.x * LDT;
-            for (int m = 0; m < SR; ++m) bacc += to_f(zr[m]);
-        }
-        __syncthreads();
-    }
-    float* part = a.part + (int64_t)blockIdx.x * a.G;
-    if (active) {
+        for (int j = 0; j < C::MTW; ++j)
+            fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
 #pragma unroll
         for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
-            for (int j = 0; j < C::MTW; ++j) {
-                const int kc = job.kb * H + (mt0 + j) * 16 + (lane & 15);
+            for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
+        if (do_bias) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int n = (nt0 + i) * 16 + (lane >> 4) * 4 + r;
-                    if (n < job.n && kc < job.k) part[job.w_off + (int64_t)n * job.k + kc] = acc[i][j][r];
+            for (int i = 0; i < C::NTW; ++i) {
+                if constexpr (VEC == 1) {
+                    bsum[i] += to_f(fa[i]);
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) bsum[i] += (float)fa[i][v];
                 }
             }
+        }
     }
-    if (job.b_off >= 0 && threadIdx.x < job.n) part[job.b_off + threadIdx.x] = bacc;
+    float* part = a.part + (int64_t)blockIdx.x * a.G;
+#pragma unroll
+    for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j) {
+            const int kc = col0 + (mt0 + j) * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = (nt0 + i) * 16 + (lane >> 4) * 4 + r;
+                if (n < job.n && kc < job.k) part[job.w_off + (int64_t)n * job.k + kc] = acc[i][j][r];
+            }
+        }
+    if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i) {
+            float t = bsum[i];
+            t += __shfl_xor(t, 16);
+            t += __shfl_xor(t, 32);
+            const int n = (nt0 + i) * 16 + lane;
+            if (lane < 16 && n < job.n) part[job.b_off + n] = t;
+        }
+    }
 }
 
-// grads[g] = Σ_c part[c][g] (g < G);  grads[G + s] = Σ_t dscale_part[t][s] (s < NS)
+// grads[g] = Σ_c part[c][g] for g < G (blocks [0, ceil(G/64)): 64 outputs x 4 chunk groups each);
+// grads[G + s] = Σ_t dscale_part[t][s] (one block per s). Fixed summation order: deterministic.
 __global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(const float* __restrict__ part, int nchunks,
                                                                    int64_t G, const float* __restrict__ dsp,
                                                                    int ntiles, int NS, float* __restrict__ grads) {
-    const int64_t g = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x;
-    if (g < G) {
+    __shared__ float red[MGN_THREADS];
+    const int64_t gblocks = (G + 63) / 64;
+    const int tid = threadIdx.x;
+    if ((int64_t)blockIdx.x < gblocks) {
+        const int64_t g = (int64_t)blockIdx.x * 64 + (tid & 63);
+        const int cg = tid >> 6;
         float s = 0.f;
-        for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * G + g];
-        grads[g] = s;
-    } else if (g < G + NS) {
-        const int sidx = (int)(g - G);
+        if (g < G) {
+            int c = cg;
+            for (; c + 12 < nchunks; c += 16) {
+                const float v0 = part[(int64_t)c * G + g], v1 = part[(int64_t)(c + 4) * G + g];
+                const float v2 = part[(int64_t)(c + 8) * G + g], v3 = part[(int64_t)(c + 12) * G + g];
+                s += v0;
+                s += v1;
+                s += v2;
+                s += v3;
+            }
+            for (; c < nchunks; c += 4) s += part[(int64_t)c * G + g];
+        }
+        red[tid] = s;
+        __syncthreads();
+        if (tid < 64 && g < G) grads[g] = ((red[tid] + red[tid + 64]) + red[tid + 128]) + red[tid + 192];
+    } else {
+        const int sidx = (int)(blockIdx.x - gblocks);
         float s = 0.f;
-        for (int t = 0; t < ntiles; ++t) s += dsp[(int64_t)t * NS + sidx];
-        grads[g] = s;
+        for (int t = tid; t < ntiles; t += MGN_THREADS) s += dsp[(int64_t)t * NS + sidx];
+        red[tid] = s;
+        __syncthreads();
+        for (int w = MGN_THREADS / 2; w > 0; w >>= 1) {
+            if (tid < w) red[tid] += red[tid + w];
+            __syncthreads();
+        }
+        if (tid == 0) grads[G + sidx] = red[0];
     }
 }
 
@@ -802,14 +803,17 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     a.out_dtype = out_dtype;
     a.out_ld = out_ld;
     a.resid = resid;
-    a.act_save = sv->act;
+    a.act8 = sv->act;
+    for (int l = 0; l < m->n_layers; ++l) a.act_off[l] = act_off(*m, M, l);
+    a.mask = reinterpret_cast<unsigned long long*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
     a.z_save = sv->z;
     a.rden_save = sv->rden;
     const size_t in_elems = (size_t)BM * (a.ldi > a.ldh ? a.ldi : a.ldh);
     const size_t lds = (in_elems + (size_t)BM * a.ldh) * sizeof(T) + 4 * BM * sizeof(float);
     auto fn = mlp_fwd_kernel<T, H, BM, MODE>;
     if (int e = set_lds((const void*)fn, lds)) return e;
-    const int grid = (int)cdiv64(M, BM);
+    const int grid = (int)(rows_pad(M) / BM);
     if (grid == 0) return 0;
     ProfScope ps(MODE == MODE_EDGE ? PROF_FWD_EDGE : MODE == MODE_NODE ? PROF_FWD_NODE : PROF_FWD_DENSE, st);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
@@ -845,7 +849,8 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     a.dinv = (float)(1.0 / sqrt((double)m->out_dim));
     a.wtpack = m->wtpack;
     a.scale = m->scale;
-    a.act_save = sv->act;
+    a.mask = reinterpret_cast<const unsigned long long*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
     a.z_save = sv->z;
     a.rden_save = sv->rden;
     a.dout = dout;
@@ -853,7 +858,8 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     a.dout_ld = dout_ld;
     a.gath = o.gath;
     a.gath_idx = o.gath_idx;
-    a.dz_save = dz_save;
+    a.dz8 = dz_save;
+    a.RP = rows_pad(M);
     a.dscale_part = dscale_part;
     a.din = o.din;
     a.din_dtype = o.din_dtype;
@@ -863,7 +869,7 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     const size_t lds = 2 * (size_t)BM * a.ldh * sizeof(T) + MGN_THREADS * 4 * sizeof(float);
     auto fn = mlp_bwd_kernel<T, H, BM, MODE>;
     if (int e = set_lds((const void*)fn, lds)) return e;
-    const int grid = (int)cdiv64(M, BM);
+    const int grid = (int)(rows_pad(M) / BM);
     if (grid == 0) return 0;
     ProfScope ps(MODE == MODE_EDGE ? PROF_BWD_EDGE : MODE == MODE_NODE ? PROF_BWD_NODE : PROF_BWD_DENSE, st);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
@@ -882,29 +888,29 @@ int64_t grad_G(const mgn_mlp* m) {
     return g;
 }
 
+int wgrad_jobs(const mgn_mlp* m) { return cdiv(m->in_dim, m->hidden) + (m->n_layers - 1); }
+
+// rows per chunk: enough workgroups to fill the chip (~512), at most 64 partial slabs
 int wgrad_rows_per_chunk(const mgn_mlp* m, int64_t M) {
-    const int H = m->hidden;
-    int jobs = cdiv(m->in_dim, H) + (m->n_layers - 1);
-    int64_t target = 1024 / jobs;
-    if (target < 1) target = 1;
-    int64_t r = cdiv64(M, target);
+    const int64_t RP = rows_pad(M);
+    int64_t chunks = cdiv64(512, wgrad_jobs(m));
+    if (chunks > 64) chunks = 64;
+    int64_t r = cdiv64(RP, chunks);
     r = cdiv64(r, 64) * 64;
-    if (r < 256) r = 256;
+    if (r < 64) r = 64;
     return (int)r;
 }
 
 template <class T, int H>
-int launch_wgrad(const mgn_mlp* m, int64_t M, const MlpIn& in, const void* act_save, const void* dz_save,
-                 const float* dscale_part, int ntiles, float* part, float* grads, hipStream_t st) {
+int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8, const float* dscale_part,
+                 int ntiles, float* part, float* grads, hipStream_t st) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
-    a.M = M;
+    a.RP = rows_pad(M);
     a.H = H;
     a.rows_per_chunk = wgrad_rows_per_chunk(m, M);
-    a.dz_save = dz_save;
-    a.act_save = act_save;
-    for (int s = 0; s < in.nseg; ++s) a.seg[s] = in.seg[s];
-    a.nseg = in.nseg;
+    a.dz8 = dz8;
+    a.act8 = act8;
     a.part = part;
     a.G = grad_G(m);
     int nj = 0;
@@ -914,32 +920,31 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const MlpIn& in, const void* act_s
         mlp_layer_shape(*m, l, &n, &k);
         for (int kb = 0; kb < cdiv(k, H); ++kb) {
             MGN_REQUIRE(nj < 12, "too many weight-gradient jobs");
-            a.job[nj].layer = l;
-            a.job[nj].kb = kb;
-            a.job[nj].n = n;
-            a.job[nj].k = k;
-            a.job[nj].w_off = off;
-            a.job[nj].b_off = kb == 0 ? off + (int64_t)n * k : -1;
-            ++nj;
+            WgJob& j = a.job[nj++];
+            j.layer = l;
+            j.kb = kb;
+            j.n = n;
+            j.k = k;
+            j.kp = act_cols(*m, l);
+            j.w_off = off;
+            j.b_off = kb == 0 ? off + (int64_t)n * k : -1;
+            j.act_off = act_off(*m, M, l);
         }
         off += (int64_t)n * k + n;
     }
     a.njobs = nj;
-    const int nchunks = (int)cdiv64(M, a.rows_per_chunk);
-    constexpr int LDT = 64 + 16 / sizeof(T);
-    const size_t lds = 2 * (size_t)H * LDT * sizeof(T);
+    const int nchunks = (int)cdiv64(a.RP, a.rows_per_chunk);
     auto fn = mlp_wgrad_kernel<T, H>;
-    if (int e = set_lds((const void*)fn, lds)) return e;
     if (nchunks > 0) {
         ProfScope ps(PROF_WGRAD, st);
-        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
+        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), 0, st, a);
         MGN_LAUNCH_CHECK();
     }
     ProfScope ps2(PROF_WGRAD_REDUCE, st);
     const int NS = m->has_norm ? m->out_dim : 0;
-    const int64_t tot = a.G + NS;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)cdiv64(tot, MGN_THREADS)), dim3(MGN_THREADS), 0, st,
-                       (const float*)part, nchunks, a.G, dscale_part, ntiles, NS, grads);
+    const unsigned blocks = (unsigned)(cdiv64(a.G, 64) + NS);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, (const float*)part, nchunks,
+                       a.G, dscale_part, ntiles, NS, grads);
     MGN_LAUNCH_CHECK();
     return 0;
 }
@@ -949,9 +954,9 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
     const int BM = m->dtype == MGN_F32 ? 32 : 64;
-    const int64_t ntiles = cdiv64(M, BM);
-    const int64_t nchunks = cdiv64(M, wgrad_rows_per_chunk(m, M));
-    size_t b = align_up((size_t)m->n_layers * M * m->hidden * es);          // dz_save
+    const int64_t ntiles = rows_pad(M) / BM;
+    const int64_t nchunks = cdiv64(rows_pad(M), wgrad_rows_per_chunk(m, M));
+    size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
     b += align_up((size_t)nchunks * grad_G(m) * sizeof(float));              // wgrad partial slabs
     return b;
@@ -1004,13 +1009,13 @@ static int mlp_bwd_any(const mgn_mlp* m, int mode, int64_t M, const mgn_mlp_save
     return rc;
 }
 
-static int mlp_wgrad_any(const mgn_mlp* m, int64_t M, const MlpIn& in, const void* act, const void* dz,
-                         const float* dsp, int ntiles, float* part, float* grads, hipStream_t st) {
+static int mlp_wgrad_any(const mgn_mlp* m, int64_t M, const void* act, const void* dz, const float* dsp,
+                         int ntiles, float* part, float* grads, hipStream_t st) {
     int rc = 0;
     if (m->dtype == MGN_F32) {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, in, act, dz, dsp, ntiles, part, grads, st)))
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, act, dz, dsp, ntiles, part, grads, st)))
     } else {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, in, act, dz, dsp, ntiles, part, grads, st)))
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, act, dz, dsp, ntiles, part, grads, st)))
     }
     return rc;
 }
@@ -1022,10 +1027,10 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
     MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, M), "backward workspace too small");
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
     const int BM = m->dtype == MGN_F32 ? 32 : 64;
-    const int ntiles = (int)cdiv64(M, BM);
+    const int ntiles = (int)(rows_pad(M) / BM);
     char* p = reinterpret_cast<char*>(ws);
     void* dz = p;
-    p += align_up((size_t)m->n_layers * M * m->hidden * es);
+    p += align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);
     float* dsp = reinterpret_cast<float*>(p);
     p += align_up((size_t)ntiles * m->out_dim * sizeof(float));
     float* part = reinterpret_cast<float*>(p);
@@ -1034,7 +1039,8 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
         return 0;
     }
     if (int e = mlp_bwd_any(m, mode, M, sv, dout, dout_dtype, dout_ld, o, dz, dsp, st)) return e;
-    return mlp_wgrad_any(m, M, in, sv->act, dz, dsp, ntiles, part, grads, st);
+    (void)in;
+    return mlp_wgrad_any(m, M, sv->act, dz, dsp, ntiles, part, grads, st);
 }
 
 // =========================================================================== node combine
@@ -1098,7 +1104,8 @@ int mgn_pack_weights(const mgn_pack_job* jobs, int32_t njobs, int64_t max_elems,
 int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
                     int64_t rows, void* out, int32_t out_dtype, mgn_mlp_saved* saved, mgn_stream_t stream) {
     if (int e = check_mlp(m)) return e;
-    MGN_REQUIRE(saved && saved->act && (!m->has_norm || (saved->z && saved->rden)), "saved buffers missing");
+    MGN_REQUIRE(saved && saved->act && (m->n_layers < 2 || saved->mask) && (!m->has_norm || (saved->z && saved->rden)),
+                "saved buffers missing");
     MGN_REQUIRE(in_dtype == MGN_F32 || in_dtype == m->dtype, "input dtype must be fp32 or the MLP dtype");
     MlpIn mi;
     memset(&mi, 0, sizeof(mi));
@@ -1109,6 +1116,12 @@ int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t 
 }
 
 size_t mgn_mlp_backward_workspace_bytes(const mgn_mlp* m, int64_t rows) { return mlp_bwd_ws(m, rows); }
+
+int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int64_t* act_elems, int64_t* mask_words) {
+    *act_elems = act_off(*m, rows, m->n_layers);
+    *mask_words = (int64_t)(m->n_layers - 1) * mask_words_per_layer(*m, rows);
+    return 0;
+}
 
 int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
                      int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,

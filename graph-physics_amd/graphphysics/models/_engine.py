@@ -211,18 +211,21 @@ def _empty(n, dtype, device):
     return torch.empty(max(int(n), 1), dtype=dtype, device=device)
 
 
-def _alloc_mlp_saved(spec, rows, tdt, device, need_z):
-    act = _empty((spec.n_layers - 1) * rows * spec.hidden, tdt, device)
+def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z):
+    ae, mw = ctypes.c_int64(), ctypes.c_int64()
+    nat.check(nat.lib().mgn_mlp_saved_elems(ctypes.byref(desc), rows, ctypes.byref(ae), ctypes.byref(mw)))
+    act = _empty(ae.value, tdt, device)
+    mask = _empty(mw.value, torch.int64, device)
     z = _empty(rows * spec.hidden, tdt, device) if need_z else None
     rden = _empty(rows, torch.float32, device) if need_z else None
-    s = nat.MlpSaved(act.data_ptr(), z.data_ptr() if z is not None else 0,
+    s = nat.MlpSaved(act.data_ptr(), mask.data_ptr(), z.data_ptr() if z is not None else 0,
                      rden.data_ptr() if rden is not None else 0)
-    return s, (act, z, rden)
+    return s, (act, mask, z, rden)
 
 
-def _alloc_block_saved(espec, nspec, topo, tdt, device):
-    se, ke = _alloc_mlp_saved(espec, topo.num_edges, tdt, device, True)
-    sn, kn = _alloc_mlp_saved(nspec, topo.num_nodes, tdt, device, nspec.norm is not None)
+def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device):
+    se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True)
+    sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None)
     aggr = _empty(topo.num_nodes * espec.hidden, tdt, device)
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
 
@@ -290,8 +293,8 @@ class EPDFunction(torch.autograd.Function):
             ein = edge_attr.detach().float().contiguous()
             x0 = torch.empty((N, H), dtype=tdt, device=dev)
             e0 = torch.empty((E, H), dtype=tdt, device=dev)
-            sv_ne = _alloc_mlp_saved(ne, N, tdt, dev, ne.norm is not None)
-            sv_ee = _alloc_mlp_saved(ee, E, tdt, dev, ee.norm is not None)
+            sv_ne = _alloc_mlp_saved(descs[0], ne, N, tdt, dev, ne.norm is not None)
+            sv_ee = _alloc_mlp_saved(descs[1], ee, E, tdt, dev, ee.norm is not None)
             _mlp_fwd(descs[0], ne, xin, nat.MGN_F32, ne.in_dim, None, N, x0, mdt, sv_ne[0], st)
             _mlp_fwd(descs[1], ee, ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, e0, mdt, sv_ee[0], st)
         xs, es, svs = [x0], [e0], []
@@ -300,7 +303,7 @@ class EPDFunction(torch.autograd.Function):
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
             if train or scratch is None:
-                sv = _alloc_block_saved(es_, ns_, topo, tdt, dev)
+                sv = _alloc_block_saved(bdescs[2 * b], bdescs[2 * b + 1], es_, ns_, topo, tdt, dev)
                 if not train:
                     scratch = sv
             else:
@@ -320,7 +323,7 @@ class EPDFunction(torch.autograd.Function):
             out = xs[-1].float()
         else:
             out = torch.empty((N, dec.out_dim), dtype=torch.float32, device=dev)
-            sv_dec = _alloc_mlp_saved(dec, N, tdt, dev, dec.norm is not None)
+            sv_dec = _alloc_mlp_saved(descs[2], dec, N, tdt, dev, dec.norm is not None)
             _mlp_fwd(descs[2], dec, xs[-1], mdt, H, None, N, out, nat.MGN_F32, sv_dec[0], st)
         if train:
             ctx.plan, ctx.mdt, ctx.only_processor, ctx.topo = plan, mdt, only_processor, topo
@@ -408,7 +411,7 @@ class BlockFunction(torch.autograd.Function):
         e0 = _permute(edge_attr.detach().contiguous(), topo.csc_eid, E, H,
                       nat.mgn_dtype(edge_attr.dtype) if edge_attr.dtype in (torch.float32, torch.bfloat16)
                       else nat.MGN_F32, tdt, False, st) if E else torch.empty((0, H), dtype=tdt, device=dev)
-        sv = _alloc_block_saved(espec, nspec, topo, tdt, dev)
+        sv = _alloc_block_saved(pw.descs[0], pw.descs[1], espec, nspec, topo, tdt, dev)
         x1 = torch.empty((N, H), dtype=tdt, device=dev)
         e1 = torch.empty((max(E, 1), H), dtype=tdt, device=dev)
         nat.check(nat.lib().mgn_block_forward(

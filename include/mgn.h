@@ -89,11 +89,18 @@ typedef struct mgn_mlp {
     const float* scale;                /* fp32 RMSNorm scale [out_dim] or NULL                */
 } mgn_mlp;
 
+/* Forward state kept for the backward. `act` holds the INPUT of every Linear (layer 0: the
+ * gathered/concatenated MLP input; layer l>0: the ReLU output of layer l-1) in the row-octet
+ * layout (element (m,c) at ((m/8)*cols + c)*8 + m%8, rows padded to 64) that makes every weight-
+ * gradient MFMA fragment one 16-byte load; `mask` holds the hidden layers' ReLU masks as 64-bit
+ * wave-ballot words. Sizes: mgn_mlp_saved_elems(). */
 typedef struct mgn_mlp_saved {
-    void* act;    /* [(n_layers-1), M, hidden] post-ReLU activations (dtype)                  */
-    void* z;      /* [M, out_dim] last Linear output before RMSNorm (dtype); unused w/o norm  */
-    float* rden;  /* [M] RMSNorm denominator rms+eps                                          */
+    void* act;    /* act_elems elements of dtype                                             */
+    void* mask;   /* mask_words x 8 bytes                                                    */
+    void* z;      /* [M, hidden] last Linear output before RMSNorm (dtype); NULL w/o norm    */
+    float* rden;  /* [M] RMSNorm denominator rms+eps; NULL w/o norm                          */
 } mgn_mlp_saved;
+int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int64_t* act_elems, int64_t* mask_words);
 
 /* Pack job: one nn.Linear weight [n, k] fp32 row-major → fragment buffers (dtype). */
 typedef struct mgn_pack_job {
