@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU baseline steps (0: skip)")
     ap.add_argument("--no-mse", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     return ap.parse_args()
 
 
@@ -75,11 +76,10 @@ def main():
     from graphphysics import _native as nat
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.models.simulator import Simulator
-    from graphphysics.training.distributed import allreduce_gradients, global_masked_mse
     from graphphysics.training.optim import FusedAdamW
+    from graphphysics.training.step import TrainStep
     from graphphysics.utils import meshes
     from graphphysics.utils.data import Data
-    from graphphysics.utils.loss import L2Loss
     from graphphysics.utils.nodetype import NodeType
     from graphphysics.utils.scheduler import CosineWarmupScheduler
 
@@ -94,35 +94,20 @@ def main():
     torch.manual_seed(0)
     model = EncodeProcessDecode(a.mp, 2 + NodeType.SIZE, 3, 2, a.hidden, compute_dtype=cdt)
     sim = Simulator(2 + NodeType.SIZE, 3, 2, 0, 2, 0, 2, 2, model, dev)
-    if world > 1:
-        sim.set_process_group(dist.group.WORLD)
     params = list(sim.parameters())
     opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
     sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
-    masks = [NodeType.NORMAL, NodeType.OUTFLOW]
-    l2 = L2Loss()
-    node_type = data.x[:, 2]
-
-    def step():
-        net, tdn, _ = sim(data)
-        loss = global_masked_mse(tdn, net, node_type, masks) if world > 1 else \
-            l2(tdn, net, node_type, masks)
-        loss.backward()
-        if world > 1:
-            allreduce_gradients(params)
-        opt.step()
-        sched.step()
-        opt.zero_grad(set_to_none=True)
-        return loss
-
     sim.train()
-    for _ in range(a.warmup):
-        step()
+    step = TrainStep(sim, opt, sched, data, graph=not a.no_graph)
+    if step.use_graph:
+        step.capture(warmup=max(a.warmup - 1, 1))
+        step()  # first replay
+    else:
+        for _ in range(a.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not a.no_profile:
-        nat.profile_enable(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -131,8 +116,16 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    prof = nat.profile_collect() if not a.no_profile else {}
-    nat.profile_enable(False)
+    prof = {}
+    if not a.no_profile:
+        # Per-kernel durations: HIP events on the launch stream around every kernel of K more steps
+        # run eagerly (the same kernels, shapes and launch order the replayed graph contains).
+        nat.profile_enable(True)
+        for _ in range(a.steps):
+            step.eager()
+        torch.cuda.synchronize()
+        prof = nat.profile_collect()
+        nat.profile_enable(False)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -171,6 +164,7 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
         "data": "synthetic: %d jittered copies of the reference in-tree CylinderFlow mesh per GPU, "
                 "random-init weights (seed 0)" % a.batch,
+        "execution": "hipGraph replay of the whole step" if step.use_graph else "eager",
         "config": {"workload": "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, h, a.batch),
                    "nodes_per_gpu": N, "edges_per_gpu": E, "global_batch": a.batch * world,
                    "parallelism": "dp%d" % world, "graphs_per_sec": round(value * a.batch, 2)},

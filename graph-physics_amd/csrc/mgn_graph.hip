@@ -105,9 +105,48 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     }
 }
 
+// Same update with lr and step read from device memory (double[2] = {lr, step}) so a captured
+// hipGraph replays correct schedules: the host refreshes the two doubles before each replay.
+__global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        const double* __restrict__ hyper, double beta1,
+                                                        double beta2, double eps, double wd) {
+#pragma clang fp contract(off)
+    const double lr = hyper[0], step = hyper[1];
+    const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
+    const float decay = (float)(1.0 - lr * wd), w1 = (float)(1.0 - beta1), b2 = (float)beta2;
+    const float omb2 = (float)(1.0 - beta2), bc2s = (float)sqrt(bc2), epsf = (float)eps;
+    const float neg_step = (float)(-(lr / bc1));
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float pi = p[i] * decay;
+        const float gi = g[i];
+        float mi = fmaf(w1, gi - m[i], m[i]);
+        float vi = v[i] * b2;
+        vi = vi + (omb2 * gi) * gi;
+        const float den = sqrtf(vi) / bc2s + epsf;
+        pi = pi + neg_step * (mi / den);
+        p[i] = pi;
+        m[i] = mi;
+        v[i] = vi;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  const double* hyper, double beta1, double beta2, double eps, double weight_decay,
+                  mgn_stream_t stream) {
+    if (n == 0) return 0;
+    int64_t blocks = cdiv64(n, 256);
+    if (blocks > 4096) blocks = 4096;
+    ProfScope ps(PROF_ADAMW, (hipStream_t)stream);
+    hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
+                       exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
 
 int mgn_abi_version(void) { return MGN_ABI_VERSION; }
 const char* mgn_last_error(void) { return g_err.c_str(); }

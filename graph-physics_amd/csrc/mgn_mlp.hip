@@ -13,8 +13,10 @@
 //               (layers.py:698-699), saved activations for the backward.
 // Backward = data-gradient chain per tile (same structure, transposed weight fragments) +
 // weight-gradient GEMMs over row chunks (K = rows) with a fixed-order partial-slab reduction.
-#include <cstring>
 #include <cmath>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "mgn_common.h"
 
@@ -738,9 +740,16 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 template <class T>
 constexpr int bm_of() { return sizeof(T) == 4 ? 32 : 64; }
 
+// Raise a kernel's dynamic-LDS limit once (not per launch: launches may be inside a graph capture).
 int set_lds(const void* fn, size_t bytes) {
-    if (bytes > 65536)
-        MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    if (bytes <= 65536) return 0;
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> done;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find(fn);
+    if (it != done.end() && it->second >= bytes) return 0;
+    MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done[fn] = bytes;
     return 0;
 }
 

@@ -70,6 +70,7 @@ EXPORTS = {
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
+    "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
     "mgn_profile_enable": (_i32, [_i32]),
     "mgn_profile_collect": (_i32, [_i32, _vp, _vp]),
 }

@@ -89,7 +89,7 @@ class Normalizer(nn.Module):
     def _accumulate(self, d: torch.Tensor):
         s = torch.sum(d, dim=0, keepdim=True)
         s2 = torch.sum(d ** 2, dim=0, keepdim=True)
-        cnt = torch.tensor(float(d.shape[0]), device=d.device)
+        cnt = torch.full((), float(d.shape[0]), device=d.device)
         if self.process_group is not None:
             import torch.distributed as dist
 
@@ -105,12 +105,10 @@ class Normalizer(nn.Module):
         self._num_accumulations += live.float()
 
     def _mean(self) -> torch.Tensor:
-        safe = torch.max(self._acc_count, torch.tensor(1.0, device=self._acc_count.device))
-        return self._acc_sum / safe
+        return self._acc_sum / self._acc_count.clamp(min=1.0)  # = torch.max(count, 1.0)
 
     def _std_with_epsilon(self) -> torch.Tensor:
-        safe = torch.max(self._acc_count, torch.tensor(1.0, device=self._acc_count.device))
-        var = self._acc_sum_squared / safe - self._mean() ** 2
+        var = self._acc_sum_squared / self._acc_count.clamp(min=1.0) - self._mean() ** 2
         std = torch.sqrt(torch.clamp(var, min=0.0))
         return torch.max(std, self._std_epsilon.to(std.device))
 

@@ -12,18 +12,24 @@ Gradients of EncodeProcessDecode live in one flat buffer, so (3) is a single all
 import torch
 import torch.distributed as dist
 
-from graphphysics.utils.loss import _prepare_mask_for_loss
+from graphphysics.utils.loss import _prepare_mask_for_loss, masked_mse
 
 
-def global_masked_mse(target, network_output, node_type, masks, group=None):
-    """L2Loss (reference utils/loss.py:28-65) over the union of all ranks' nodes: returns the local
-    contribution Σ_local err² / N_global, whose sum over ranks is the global masked mean."""
-    mask = _prepare_mask_for_loss(network_output, node_type, masks)
-    err = ((network_output - target) ** 2)[mask]
-    cnt = torch.tensor([float(err.numel())], device=err.device)
+def global_mask_count(node_type, masks, group=None, dtype=torch.float32):
+    """Number of loss-masked nodes over all ranks (one tiny all-reduce)."""
+    cnt = _prepare_mask_for_loss(node_type[:, None], node_type, masks).to(dtype).sum().reshape(1)
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(cnt, group=group)
-    return err.sum() / cnt[0]
+    return cnt[0]
+
+
+def global_masked_mse(target, network_output, node_type, masks, group=None, count=None):
+    """L2Loss (reference utils/loss.py:28-65) over the union of all ranks' nodes: the local
+    contribution Σ_local err² / (N_global · n_out); summed over ranks it is the global masked mean,
+    so SUM-all-reduced gradients are the gradients of the single-process loss."""
+    if count is None:
+        count = global_mask_count(node_type, masks, group, network_output.dtype)
+    return masked_mse(target, network_output, node_type, masks, count=count)
 
 
 def flat_grad_buffer(params):

@@ -1,11 +1,13 @@
-"""Fused AdamW on MI355X: one mgn_adamw launch over the flat parameter buffer.
+"""Fused AdamW on MI355X: one mgn_adamw_dev launch over the flat parameter buffer.
 
 Semantics of torch.optim.AdamW as the reference configures it (reference
 graphphysics/training/lightning_module.py:275-292: lr, weight_decay=1e-4, betas=(0.9, 0.95),
 eps=1e-8): decoupled decay p *= 1 - lr*wd, exp_avg lerp, exp_avg_sq, bias-corrected step.
 When the parameters and their gradients are consecutive views of one buffer each (what
 EncodeProcessDecode sets up), the whole model is updated by a single kernel; otherwise one launch
-per parameter. Parameters must live on a HIP device.
+per parameter. lr and the step count live in a device buffer ({lr, step} doubles), refreshed by
+stage() on the host side of each step, so launch() can be captured in a hipGraph.
+Parameters must live on a HIP device.
 """
 import torch
 
@@ -13,7 +15,7 @@ from graphphysics import _native as nat
 
 
 def _flat_span(tensors):
-    """If tensors are consecutive, contiguous views of one storage, return (base_tensor_view)."""
+    """If tensors are consecutive, contiguous fp32 views of one storage, return that span."""
     if not tensors:
         return None
     t0 = tensors[0]
@@ -39,34 +41,50 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        L = nat.lib()
+        self.stage()
+        self.launch()
+        return loss
+
+    @torch.no_grad()
+    def stage(self):
+        """Host side of a step: advance the step count and write {lr, step} to the device."""
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
-            for p in ps:
-                nat.require_device(p)
-            b1, b2 = group["betas"]
             if "flat_state" not in group or group.get("flat_members") != [id(p) for p in ps]:
                 self._init_state(group, ps)
             group["step_count"] = group.get("step_count", 0) + 1
-            step = group["step_count"]
+            hyper = group["hyper"]
+            hyper[0].fill_(float(group["lr"]))
+            hyper[1].fill_(float(group["step_count"]))
+            for p in ps:
+                self.state[p]["step"] = torch.tensor(float(group["step_count"]))
+
+    @torch.no_grad()
+    def launch(self):
+        """Device side of a step (graph-capturable): the AdamW kernel(s)."""
+        L = nat.lib()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps or "flat_state" not in group:
+                continue
+            for p in ps:
+                nat.require_device(p)
+            b1, b2 = group["betas"]
             st = nat.stream_ptr(ps[0].device)
+            hyper = group["hyper"]
             fp, fg = _flat_span(ps), _flat_span([p.grad for p in ps])
             fm, fv = group["flat_state"]
             if fp is not None and fg is not None:
-                nat.check(L.mgn_adamw(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
-                                      group["lr"], b1, b2, group["eps"], group["weight_decay"], step, st))
+                nat.check(L.mgn_adamw_dev(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
+                                          nat.ptr(hyper), b1, b2, group["eps"], group["weight_decay"], st))
             else:
                 for p in ps:
                     s = self.state[p]
-                    g = p.grad.contiguous()
-                    nat.check(L.mgn_adamw(nat.ptr(p), nat.ptr(g), nat.ptr(s["exp_avg"]),
-                                          nat.ptr(s["exp_avg_sq"]), p.numel(), group["lr"], b1, b2,
-                                          group["eps"], group["weight_decay"], step, st))
-            for p in ps:
-                self.state[p]["step"] = torch.tensor(float(step))
-        return loss
+                    nat.check(L.mgn_adamw_dev(nat.ptr(p), nat.ptr(p.grad.contiguous()), nat.ptr(s["exp_avg"]),
+                                              nat.ptr(s["exp_avg_sq"]), p.numel(), nat.ptr(hyper), b1, b2,
+                                              group["eps"], group["weight_decay"], st))
 
     def _init_state(self, group, ps):
         n = sum(p.numel() for p in ps)
@@ -86,3 +104,4 @@ class FusedAdamW(torch.optim.Optimizer):
             o += k
         group["flat_state"] = (fm, fv)
         group["flat_members"] = [id(p) for p in ps]
+        group["hyper"] = torch.zeros(2, dtype=torch.float64, device=dev)

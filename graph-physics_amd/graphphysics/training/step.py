@@ -1,0 +1,84 @@
+"""One MGN training step, optionally captured as a hipGraph.
+
+Semantics = the reference's LightningModule.training_step + Lightning automatic optimisation
+(reference graphphysics/training/lightning_module.py:111-122, 275-292): Simulator train forward
+(normalizer accumulation, one-hot, EncodeProcessDecode) → masked L2 loss over NORMAL ∪ OUTFLOW
+nodes → backward → AdamW → cosine-warmup LR step (scheduler.py:41-67).
+
+Captured mode (single process): the whole forward + backward + AdamW launch sequence (~140 kernels)
+is recorded once into a hipGraph and replayed; per step the host only writes {lr, step} to the
+device and calls replay(), so host/launch overhead disappears. Requires a static batch (the bench's
+resident synthetic meshes, or a training loop that copies each batch into the same buffers).
+Data parallel (process group of >1 rank): eager step with the three exchanges of
+graphphysics.training.distributed (normalizer statistics, global masked-node count, gradients).
+"""
+import torch
+import torch.distributed as dist
+
+from graphphysics.training.distributed import allreduce_gradients, global_mask_count
+from graphphysics.utils.loss import masked_mse
+from graphphysics.utils.nodetype import NodeType
+
+
+class TrainStep:
+    def __init__(self, sim, opt, sched, batch, masks=(NodeType.NORMAL, NodeType.OUTFLOW), graph=True,
+                 group=None):
+        self.sim, self.opt, self.sched, self.batch = sim, opt, sched, batch
+        self.masks = list(masks)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.node_type = batch.x[:, sim.node_type_index]
+        self.params = [p for p in sim.parameters() if p.requires_grad]
+        self.use_graph = graph and self.world == 1
+        self.graph = None
+        self.static_loss = None
+        self._count = None
+        if self.world > 1:
+            sim.set_process_group(group if group is not None else dist.group.WORLD)
+
+    def _loss(self):
+        net, tdn, _ = self.sim(self.batch)
+        return masked_mse(tdn, net, self.node_type, self.masks, count=self._count)
+
+    def eager(self):
+        self.opt.zero_grad(set_to_none=True)
+        if self.world > 1 and self._count is None:
+            self._count = global_mask_count(self.node_type, self.masks, self.group)
+        loss = self._loss()
+        loss.backward()
+        if self.world > 1:
+            allreduce_gradients(self.params, self.group)
+        self.opt.step()
+        self.sched.step()
+        return loss
+
+    def capture(self, warmup=2, on_record=None):
+        """Run `warmup` eager steps on a side stream (allocator + library state), then record."""
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(max(warmup, 1)):
+                self.eager()
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        self.opt.zero_grad(set_to_none=True)
+        if on_record is not None:
+            on_record()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._loss()
+            loss.backward()
+            self.opt.launch()
+        self.graph, self.static_loss = g, loss
+        return self
+
+    def __call__(self):
+        if not self.use_graph:
+            return self.eager()
+        if self.graph is None:
+            self.capture()
+        self.opt.stage()
+        self.graph.replay()
+        self.sched.step()
+        return self.static_loss

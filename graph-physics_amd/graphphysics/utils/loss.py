@@ -27,4 +27,14 @@ class L2Loss(_Loss):
         return torch.mean(((network_output - target) ** 2)[mask])
 
 
-__all__ = ["L2Loss", "NodeType", "_prepare_mask_for_loss"]
+def masked_mse(target, network_output, node_type, masks, count=None):
+    """Same value as L2Loss without boolean indexing (no data-dependent shapes, no host sync, so it
+    can live inside a captured hipGraph): Σ mask·err² / (Σ mask · n_out). `count` overrides the
+    denominator's mask count (data-parallel global count)."""
+    m = _prepare_mask_for_loss(network_output, node_type, masks).to(network_output.dtype)
+    err = ((network_output - target) ** 2).sum(dim=1)
+    cnt = m.sum() if count is None else count
+    return (err * m).sum() / (cnt * network_output.shape[1])
+
+
+__all__ = ["L2Loss", "NodeType", "_prepare_mask_for_loss", "masked_mse"]

@@ -165,6 +165,12 @@ int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
               double lr, double beta1, double beta2, double eps, double weight_decay,
               int64_t step, mgn_stream_t stream);
 
+/* As mgn_adamw with lr and step read from device memory: hyper = double[2] {lr, step}. The launch
+ * can be captured in a hipGraph and replayed with a new schedule (host updates hyper). */
+int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  const double* hyper, double beta1, double beta2, double eps, double weight_decay,
+                  mgn_stream_t stream);
+
 /* ---------------------------------------------------------------- opt-in profiler */
 /* Kernel classes: 0 edge-MLP fwd, 1 node-MLP fwd, 2 dense-MLP fwd, 3 edge-MLP bwd-data,
  * 4 node-MLP bwd-data, 5 dense-MLP bwd-data, 6 weight-grad, 7 weight-grad reduce,
