@@ -180,9 +180,11 @@ __host__ __device__ inline int act_cols(const mgn_mlp& m, int l) {
     const int ks = kstep_of(m.dtype);
     return l == 0 ? rup(m.in_dim, ks) : rup(m.hidden, ks);
 }
-__host__ __device__ inline int64_t act_off(const mgn_mlp& m, int64_t M, int l) {
+// gathered != 0: MLP of a GraphNetBlock, whose layer-0 input ([e‖x_i‖x_j] or [x‖aggr]) is not
+// saved (the weight-gradient kernel re-gathers it); layer 0's block then has zero size.
+__host__ __device__ inline int64_t act_off(const mgn_mlp& m, int64_t M, int l, int gathered = 0) {
     int64_t o = 0;
-    for (int j = 0; j < l; ++j) o += rows_pad(M) * act_cols(m, j);
+    for (int j = 0; j < l; ++j) o += (gathered && j == 0) ? 0 : rows_pad(M) * act_cols(m, j);
     return o;
 }
 // ReLU masks of the hidden-layer outputs: per layer, per (16-row tile, 16-col tile), 4 ballot words

@@ -24,6 +24,10 @@ namespace {
 
 enum { MODE_DENSE = 0, MODE_EDGE = 1, MODE_NODE = 2 };
 
+// Block MLPs: save the layer-0 input in R8 (true) or re-gather it in the weight-gradient kernel
+// through an LDS transpose (false: 136 MB less HBM traffic per edge block).
+constexpr bool kSaveBlockInput = false;
+
 template <int NT, int MT>
 struct TileCfg {
     static constexpr int WN = NT < 4 ? NT : 4;
@@ -42,7 +46,7 @@ struct Gemm {
     int nt0, mt0;
     bool active;
 
-    __device__ __forceinline__ void run(const T* __restrict__ wp, int KS, const T* lds, int ldl) {
+    __device__ __forceinline__ void run(const T* __restrict__ wp, int KS, const T* lds, int ldl, bool skip = false) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const int wn = wave % C::WN, wm = wave / C::WN;
         nt0 = wn * C::NTW;
@@ -52,20 +56,37 @@ struct Gemm {
         for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
             for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        if (!active) return;
+        if (!active || skip) return;
         const T* bp = lds + (size_t)(mt0 * 16 + (lane & 15)) * ldl + VEC * (lane >> 4);
         const T* ap = wp + ((size_t)nt0 * KS * 64 + lane) * VEC;
-#pragma unroll 2
-        for (int ks = 0; ks < KS; ++ks) {
-            typename Mf<T>::frag a[C::NTW], b[C::MTW];
+        // weight fragments come from L2: keep PD k-steps of them in flight (register ring with
+        // compile-time slots; the k loop is unrolled by PD so every ring index is static)
+        constexpr int PD = 4;
+        typename Mf<T>::frag ring[PD][C::NTW];
 #pragma unroll
-            for (int i = 0; i < C::NTW; ++i) a[i] = ld_frag(ap + ((size_t)i * KS + ks) * 64 * VEC);
-#pragma unroll
-            for (int j = 0; j < C::MTW; ++j) b[j] = ld_frag(bp + (size_t)j * 16 * ldl + ks * KSTEP);
+        for (int u = 0; u < PD; ++u)
 #pragma unroll
             for (int i = 0; i < C::NTW; ++i)
+                if (u < KS) ring[u][i] = ld_frag(ap + ((size_t)i * KS + u) * 64 * VEC);
+        for (int k0 = 0; k0 < KS; k0 += PD) {
 #pragma unroll
-                for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(a[i], b[j], acc[i][j]);
+            for (int u = 0; u < PD; ++u) {
+                const int ks = k0 + u;
+                if (ks >= KS) break;
+                typename Mf<T>::frag a[C::NTW], b[C::MTW];
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i) a[i] = ring[u][i];
+                if (ks + PD < KS) {
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i) ring[u][i] = ld_frag(ap + ((size_t)i * KS + ks + PD) * 64 * VEC);
+                }
+#pragma unroll
+                for (int j = 0; j < C::MTW; ++j) b[j] = ld_frag(bp + (size_t)j * 16 * ldl + ks * KSTEP);
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(a[i], b[j], acc[i][j]);
+            }
         }
     }
     __device__ __forceinline__ int n_of(int i) const { return (nt0 + i) * 16 + ((threadIdx.x & 63) >> 4) * 4; }
@@ -100,15 +121,31 @@ __device__ void load_tile(T* In, int ldi, int K0, int KP, const SrcSeg* seg, int
                          g.coff % CH == 0;
         if (vec) {
             const int cpr = g.ncols / CH;
-            for (int it = threadIdx.x; it < BM * cpr; it += MGN_THREADS) {
-                const int r = it / cpr, c = (it - r * cpr) * CH;
-                const int64_t row = row0 + r;
-                u32x4 v = {0u, 0u, 0u, 0u};
-                if (row < M) {
-                    const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
-                    v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(g.p) + sr * g.ld + c);
+            constexpr int B = 4;  // loads in flight per thread
+            for (int base = threadIdx.x; base < BM * cpr; base += MGN_THREADS * B) {
+                u32x4 v[B];
+                int64_t sr[B];
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int it = base + q * MGN_THREADS;
+                    const int64_t row = row0 + it / cpr;
+                    sr[q] = (it < BM * cpr && row < M) ? (g.idx ? (int64_t)g.idx[row] : row) : -1;
                 }
-                *reinterpret_cast<u32x4*>(In + (size_t)r * ldi + g.coff + c) = v;
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int it = base + q * MGN_THREADS;
+                    const int c = (it % cpr) * CH;
+                    v[q] = u32x4{0u, 0u, 0u, 0u};
+                    if (sr[q] >= 0) v[q] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(g.p) + sr[q] * g.ld + c);
+                }
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int it = base + q * MGN_THREADS;
+                    if (it < BM * cpr) {
+                        const int r = it / cpr, c = (it - r * cpr) * CH;
+                        *reinterpret_cast<u32x4*>(In + (size_t)r * ldi + g.coff + c) = v[q];
+                    }
+                }
             }
         } else {
             for (int it = threadIdx.x; it < BM * g.ncols; it += MGN_THREADS) {
@@ -133,6 +170,26 @@ template <class T, int BM>
 __device__ void copy_out_r8(const T* lds, int ldl, int cols, T* dst, int64_t row0) {
     constexpr int OCT = BM / 8;
     const int64_t o0 = row0 >> 3;
+    if (sizeof(T) == 2 && (cols & 3) == 0 && (ldl & 3) == 0) {
+        // item = (octet, 4 columns): 8 ds_read_b64 (one per row) -> 4 R8 chunks of 16 B
+        const int c4 = cols >> 2;
+        for (int it = threadIdx.x; it < OCT * c4; it += MGN_THREADS) {
+            const int o = it / c4, c = (it - o * c4) * 4;
+            bf16x4 rv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                rv[q] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(lds) + (size_t)(o * 8 + q) * ldl + c);
+            __bf16* p = reinterpret_cast<__bf16*>(dst) + ((o0 + o) * cols + c) * 8;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                bf16x8 w;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) w[q] = rv[q][cc];
+                *reinterpret_cast<bf16x8*>(p + cc * 8) = w;
+            }
+        }
+        return;
+    }
     for (int it = threadIdx.x; it < OCT * cols; it += MGN_THREADS) {
         const int o = it / cols, c = it - o * cols;
         float v[8];
@@ -175,15 +232,27 @@ struct FwdArgs {
     int64_t mask_stride;                 // words per hidden layer
     void* z_save;
     float* rden_save;
+    int32_t ablate;  // diagnostics only (env MGN_ABLATE): 1 gather, 2 R8 saves, 4 MFMA, 8 epilogue stores
+    int32_t r0_elems;  // LDS region 0 (layer-0 input / odd-layer activations / fp32 z staging), in T
 };
 
+// Diagnostic ablation mask for timing studies (results are wrong when nonzero).
+static int ablate_mask() {
+    const char* e = getenv("MGN_ABLATE");
+    return e ? atoi(e) : 0;
+}
+
+// Last layer: bias, RMSNorm, residual. z is staged (fp32) in LDS `zf` ([BM][H+4], aliases the
+// dead layer-0 input region), then one cooperative pass writes z, out = resid + scale*z/q and rden
+// as coalesced 16-byte row chunks.
 template <class T, int BM, class G>
-__device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float* red, int64_t row0) {
+__device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float* red, float* zf, int64_t row0) {
     using C = typename G::C;
     const int lane = threadIdx.x & 63;
     const int wn = (threadIdx.x >> 6) % C::WN;
     const float* b = a.bias[a.L - 1];
     if (a.has_norm) {
+        const int H = a.H, ldz = a.H + 4;
         float ss[C::MTW];
 #pragma unroll
         for (int j = 0; j < C::MTW; ++j) {
@@ -200,37 +269,63 @@ __device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float*
             }
             ss[j] += __shfl_xor(ss[j], 16);
             ss[j] += __shfl_xor(ss[j], 32);
-            if (g.active && lane < 16) red[wn * BM + g.m_of(j)] = ss[j];
+        }
+        __syncthreads();  // every wave is done reading the GEMM input (zf may alias it)
+        if (g.active) {
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j) {
+                if (lane < 16) red[wn * BM + g.m_of(j)] = ss[j];
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+                    *reinterpret_cast<f4*>(zf + (size_t)g.m_of(j) * ldz + g.n_of(i)) = g.acc[i][j];
+            }
         }
         __syncthreads();
-        if (!g.active) return;
-#pragma unroll
-        for (int j = 0; j < C::MTW; ++j) {
-            const int m = g.m_of(j);
+        const int cpr = H / 8;
+        for (int it = threadIdx.x; it < BM * cpr; it += MGN_THREADS) {
+            const int r = it / cpr, c = (it - r * cpr) * 8;
+            const int64_t row = row0 + r;
+            if (row >= a.M) continue;
             float tot = 0.f;
 #pragma unroll
-            for (int w = 0; w < C::WN; ++w) tot += red[w * BM + m];
+            for (int w = 0; w < C::WN; ++w) tot += red[w * BM + r];
             const float q = sqrtf(tot) * a.dinv + RMS_EPS;
-            const int64_t row = row0 + m;
-            if (row >= a.M) continue;
-            if (wn == 0 && lane < 16) a.rden_save[row] = q;
+            if (c == 0) a.rden_save[row] = q;
+            float z[8], y[8];
+            const f4 z0 = *reinterpret_cast<const f4*>(zf + (size_t)r * ldz + c);
+            const f4 z1 = *reinterpret_cast<const f4*>(zf + (size_t)r * ldz + c + 4);
+            const f4 s0 = ld4u(a.scale + c), s1 = ld4u(a.scale + c + 4);
 #pragma unroll
-            for (int i = 0; i < C::NTW; ++i) {
-                const int n = g.n_of(i);
-                const f4 s = ld4u(a.scale + n);
-                f4 z = g.acc[i][j], y;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) y[r] = s[r] * (z[r] / q);
-                st4(reinterpret_cast<T*>(a.z_save) + row * a.H + n, z);
-                if (a.resid) {
-                    const f4 x = ld4(reinterpret_cast<const T*>(a.resid) + row * a.H + n);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) y[r] = x[r] + y[r];
+            for (int v = 0; v < 4; ++v) {
+                z[v] = z0[v];
+                z[v + 4] = z1[v];
+                y[v] = s0[v] * (z0[v] / q);
+                y[v + 4] = s1[v] * (z1[v] / q);
+            }
+            if (a.resid) {
+                float x[8];
+                if constexpr (sizeof(T) == 2) {
+                    Chunk<T>::load(reinterpret_cast<const T*>(a.resid) + row * H + c, x);
+                } else {
+                    Chunk<T>::load(reinterpret_cast<const T*>(a.resid) + row * H + c, x);
+                    Chunk<T>::load(reinterpret_cast<const T*>(a.resid) + row * H + c + 4, x + 4);
                 }
-                if (a.out_dtype == MGN_F32)
-                    st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
-                else
-                    st4(reinterpret_cast<__bf16*>(a.out) + row * a.out_ld + n, y);
+#pragma unroll
+                for (int v = 0; v < 8; ++v) y[v] = x[v] + y[v];
+            }
+            T* zp = reinterpret_cast<T*>(a.z_save) + row * H + c;
+            if constexpr (sizeof(T) == 2) {
+                Chunk<T>::store(zp, z);
+            } else {
+                Chunk<T>::store(zp, z);
+                Chunk<T>::store(zp + 4, z + 4);
+            }
+            if (a.out_dtype == MGN_BF16) {
+                Chunk<__bf16>::store(reinterpret_cast<__bf16*>(a.out) + row * a.out_ld + c, y);
+            } else {
+                float* op = reinterpret_cast<float*>(a.out) + row * a.out_ld + c;
+                Chunk<float>::store(op, y);
+                Chunk<float>::store(op + 4, y + 4);
             }
         }
     } else {
@@ -267,14 +362,13 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int KP0 = rup(a.K0, KSTEP);
     T* In = reinterpret_cast<T*>(smem);
-    const int in_elems = BM * a.ldi > BM * a.ldh ? BM * a.ldi : BM * a.ldh;
-    T* P0 = In + in_elems;
+    T* P0 = In + a.r0_elems;
     T* P1 = In;  // In is dead after layer 0
     float* red = reinterpret_cast<float*>(P0 + BM * a.ldh);
     const int64_t row0 = (int64_t)blockIdx.x * BM;
 
-    load_tile<T, BM>(In, a.ldi, a.K0, KP0, a.seg, a.nseg, row0, a.M);
-    if (MODE == MODE_NODE) {
+    if (!(a.ablate & 1)) load_tile<T, BM>(In, a.ldi, a.K0, KP0, a.seg, a.nseg, row0, a.M);
+    if (MODE == MODE_NODE && !(a.ablate & 1)) {
         // aggregation: In[r][H + c] = sum over in-edges k of scale[c] * (z[k][c] / rden[k])
         constexpr int CPR = H / CH;
         const T* z = reinterpret_cast<const T*>(a.agg_z);
@@ -289,7 +383,20 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                 for (int v = 0; v < CH; ++v) s[v] = a.agg_scale ? a.agg_scale[c + v] : 1.f;
                 const int kb = a.seg_ptr[row], ke = a.seg_ptr[row + 1];
-                for (int k = kb; k < ke; ++k) {
+                int k = kb;
+                for (; k + 4 <= ke; k += 4) {
+                    float zz[4][CH], q[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        Chunk<T>::load(z + (int64_t)(k + u) * H + c, zz[u]);
+                        q[u] = a.agg_rden[k + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int v = 0; v < CH; ++v) acc[v] += s[v] * (zz[u][v] / q[u]);
+                }
+                for (; k < ke; ++k) {
                     float zz[CH];
                     Chunk<T>::load(z + (int64_t)k * H + c, zz);
                     const float q = a.agg_rden[k];
@@ -302,14 +409,16 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
         }
     }
     __syncthreads();
-    copy_out_r8<T, BM>(In, a.ldi, KP0, reinterpret_cast<T*>(a.act8) + a.act_off[0], row0);
+    // the layer-0 input of edge/node MLPs is re-gathered by the weight-gradient kernel
+    if ((MODE == MODE_DENSE || kSaveBlockInput) && !(a.ablate & 2))
+        copy_out_r8<T, BM>(In, a.ldi, KP0, reinterpret_cast<T*>(a.act8) + a.act_off[0], row0);
 
     const T* wp = reinterpret_cast<const T*>(a.wpack);
     const T* cur = In;
     int ldc = a.ldi, KS = KP0 / KSTEP, K = a.K0;
     for (int l = 0; l < a.L - 1; ++l) {
         Gemm<T, NTH, MT> g;
-        g.run(wp, KS, cur, ldc);
+        g.run(wp, KS, cur, ldc, a.ablate & 4);
         T* nxt = (l & 1) ? P1 : P0;
         if (g.active) {
             const float* b = a.bias[l];
@@ -329,7 +438,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const unsigned long long bits = __ballot(v[r] > 0.f);
-                        if ((threadIdx.x & 63) == 0) mw[r] = bits;
+                        if ((threadIdx.x & 63) == 0 && !(a.ablate & 8)) mw[r] = bits;
                     }
                 }
             }
@@ -340,7 +449,8 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
                 nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
         }
         __syncthreads();
-        copy_out_r8<T, BM>(nxt, a.ldh, rup(H, KSTEP), reinterpret_cast<T*>(a.act8) + a.act_off[l + 1], row0);
+        if (!(a.ablate & 2))
+            copy_out_r8<T, BM>(nxt, a.ldh, rup(H, KSTEP), reinterpret_cast<T*>(a.act8) + a.act_off[l + 1], row0);
         wp += linear_pack_elems(H, K, dtype_id<T>());
         cur = nxt;
         ldc = a.ldh;
@@ -349,12 +459,13 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     }
     if (a.NOUT == H) {
         Gemm<T, NTH, MT> g;
-        g.run(wp, KS, cur, ldc);
-        fwd_last_epilogue<T, BM>(g, a, red, row0);
+        g.run(wp, KS, cur, ldc, a.ablate & 4);
+        if (a.ablate & 8) return;
+        fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
     } else {
         Gemm<T, 1, MT> g;
         g.run(wp, KS, cur, ldc);
-        fwd_last_epilogue<T, BM>(g, a, red, row0);
+        fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
     }
 }
 
@@ -405,47 +516,64 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         f4 dsc = {0.f, 0.f, 0.f, 0.f};
         f4 s = {1.f, 1.f, 1.f, 1.f};
         if (a.has_norm) s = ld4u(a.scale + cc);
-        for (int r = rr; r < BM; r += RPP) {
-            const int64_t row = row0 + r;
-            f4 dy = {0.f, 0.f, 0.f, 0.f};
-            const bool valid = row < a.M && rr < RPP;
-            if (valid) {
+        // passes of RPP rows, 4 passes per batch: all loads of a batch are issued before use
+        constexpr int MAXP = BM / 8 > 4 ? BM / 8 : 4;
+        for (int p0 = 0; p0 < MAXP; p0 += 4) {
+            f4 dy[4], z[4];
+            float q[4];
+            bool valid[4];
+            int64_t gi[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = rr + (p0 + u) * RPP;
+                valid[u] = r < BM && row0 + r < a.M;
+                gi[u] = (MODE == MODE_EDGE && valid[u]) ? (int64_t)a.gath_idx[row0 + r] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t row = row0 + rr + (p0 + u) * RPP;
+                dy[u] = f4{0.f, 0.f, 0.f, 0.f};
+                z[u] = f4{0.f, 0.f, 0.f, 0.f};
+                q[u] = 1.f;
+                if (!valid[u]) continue;
                 if (NO % 4 == 0) {
-                    dy = a.dout_dtype == MGN_F32
-                             ? ld4(reinterpret_cast<const float*>(a.dout) + row * a.dout_ld + cc)
-                             : ld4(reinterpret_cast<const __bf16*>(a.dout) + row * a.dout_ld + cc);
+                    dy[u] = a.dout_dtype == MGN_F32
+                                ? ld4(reinterpret_cast<const float*>(a.dout) + row * a.dout_ld + cc)
+                                : ld4(reinterpret_cast<const __bf16*>(a.dout) + row * a.dout_ld + cc);
                 } else {
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
-                        dy[v] = cc + v < NO ? load_any(a.dout, a.dout_dtype, row * a.dout_ld + cc + v) : 0.f;
+                        dy[u][v] = cc + v < NO ? load_any(a.dout, a.dout_dtype, row * a.dout_ld + cc + v) : 0.f;
                 }
                 if (MODE == MODE_EDGE) {
-                    const f4 g = ld4(reinterpret_cast<const T*>(a.gath) + (int64_t)a.gath_idx[row] * H + cc);
+                    const f4 g = ld4(reinterpret_cast<const T*>(a.gath) + gi[u] * H + cc);
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) dy[v] += g[v];
+                    for (int v = 0; v < 4; ++v) dy[u][v] += g[v];
+                }
+                if (a.has_norm) {
+                    z[u] = ld4(reinterpret_cast<const T*>(a.z_save) + row * H + cc);
+                    q[u] = a.rden_save[row];
                 }
             }
-            f4 dz = dy;
-            if (a.has_norm) {
-                f4 z = {0.f, 0.f, 0.f, 0.f};
-                float q = 1.f;
-                if (valid) {
-                    z = ld4(reinterpret_cast<const T*>(a.z_save) + row * H + cc);
-                    q = a.rden_save[row];
-                }
-                float dot = 0.f;
 #pragma unroll
-                for (int v = 0; v < 4; ++v) dot += s[v] * dy[v] * z[v];
-                for (int o = 1; o < CPR; o <<= 1) dot += __shfl_xor(dot, o);
-                const float rms = q - RMS_EPS;
-                const float coef = rms > 0.f ? dot / (q * q * rms) * (a.dinv * a.dinv) : 0.f;
+            for (int u = 0; u < 4; ++u) {
+                const int r = rr + (p0 + u) * RPP;
+                f4 dz = dy[u];
+                if (a.has_norm) {
+                    float dot = 0.f;
 #pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    dz[v] = s[v] * dy[v] / q - z[v] * coef;
-                    dsc[v] += dy[v] * (z[v] / q);
+                    for (int v = 0; v < 4; ++v) dot += s[v] * dy[u][v] * z[u][v];
+                    for (int o = 1; o < CPR; o <<= 1) dot += __shfl_xor(dot, o);
+                    const float rms = q[u] - RMS_EPS;
+                    const float coef = rms > 0.f ? dot / (q[u] * q[u] * rms) * (a.dinv * a.dinv) : 0.f;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        dz[v] = s[v] * dy[u][v] / q[u] - z[u][v] * coef;
+                        dsc[v] += dy[u][v] * (z[u][v] / q[u]);
+                    }
                 }
+                if (r < BM) st4(D0 + (size_t)r * a.ldh + cc, dz);
             }
-            if (r < BM) st4(D0 + (size_t)r * a.ldh + cc, dz);
         }
         // zero pad columns [NO4, max(KPN, H)) of D0
         const int NO4 = CPR * 4;
@@ -528,6 +656,38 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     for (int c = 0; c < nchunk; ++c) {
         Gemm<T, NTH, MT> g;
         g.run(wt + off[0] + (int64_t)c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+        if (MODE != MODE_DENSE) {
+            // stage the chunk in the free LDS buffer, then write coalesced 16-byte row chunks
+            if (g.active) {
+#pragma unroll
+                for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i)
+#pragma unroll
+                    for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j)
+                        st4(nxt + (size_t)g.m_of(j) * a.ldh + g.n_of(i), g.acc[i][j]);
+            }
+            __syncthreads();
+            constexpr int CH = 16 / sizeof(T);
+            for (int it = tid; it < BM * (H / CH); it += MGN_THREADS) {
+                const int r = it / (H / CH), cc = (it - r * (H / CH)) * CH;
+                const int64_t row = row0 + r;
+                if (row >= a.M) continue;
+                float v[CH];
+                Chunk<T>::load(nxt + (size_t)r * a.ldh + cc, v);
+                if (c == 0) {
+                    float d[CH];
+                    Chunk<T>::load(reinterpret_cast<const T*>(a.dout) + row * a.dout_ld + cc, d);
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) v[e] = d[e] + v[e];
+                    Chunk<T>::store(reinterpret_cast<T*>(a.o1) + row * H + cc, v);
+                } else if (MODE == MODE_EDGE) {
+                    Chunk<T>::store(reinterpret_cast<T*>(a.o2) + row * (2 * H) + (c - 1) * H + cc, v);
+                } else {
+                    Chunk<T>::store(reinterpret_cast<T*>(a.o2) + row * H + cc, v);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         if (!g.active) continue;
 #pragma unroll
         for (int i = 0; i < Gemm<T, NTH, MT>::C::NTW; ++i) {
@@ -537,24 +697,15 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
                 const int64_t row = row0 + g.m_of(j);
                 if (row >= a.M) continue;
                 const f4 v = g.acc[i][j];
-                if (MODE == MODE_DENSE) {
-                    const int k = c * H + n;
+                const int k = c * H + n;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (k + r < a.K0) {
-                            if (a.din_dtype == MGN_F32)
-                                reinterpret_cast<float*>(a.din)[row * a.din_ld + k + r] = v[r];
-                            else
-                                reinterpret_cast<__bf16*>(a.din)[row * a.din_ld + k + r] = (__bf16)v[r];
-                        }
-                } else if (c == 0) {
-                    const f4 d = ld4(reinterpret_cast<const T*>(a.dout) + row * a.dout_ld + n);
-                    st4(reinterpret_cast<T*>(a.o1) + row * H + n, d + v);
-                } else if (MODE == MODE_EDGE) {
-                    st4(reinterpret_cast<T*>(a.o2) + row * (2 * H) + (c - 1) * H + n, v);
-                } else {
-                    st4(reinterpret_cast<T*>(a.o2) + row * H + n, v);
-                }
+                for (int r = 0; r < 4; ++r)
+                    if (k + r < a.K0) {
+                        if (a.din_dtype == MGN_F32)
+                            reinterpret_cast<float*>(a.din)[row * a.din_ld + k + r] = v[r];
+                        else
+                            reinterpret_cast<__bf16*>(a.din)[row * a.din_ld + k + r] = (__bf16)v[r];
+                    }
             }
         }
     }
@@ -571,10 +722,11 @@ struct WgJob {
     int64_t w_off, b_off, act_off;  // b_off < 0: no bias for this job
 };
 struct WgArgs {
-    int64_t RP;
-    int32_t rows_per_chunk, H, njobs, pad;
+    int64_t RP, M;
+    int32_t rows_per_chunk, H, njobs, gathered, nseg, pad;
     const void* dz8;
     const void* act8;
+    SrcSeg seg[3];  // gathered != 0: layer-0 input segments (re-gathered, staged through LDS)
     WgJob job[12];
     float* part;
     int64_t G;
@@ -584,17 +736,23 @@ template <class T, int H>
 __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
     constexpr int NT = H / 16;
+    constexpr int SR = 64;                      // rows per LDS stage (re-gathered layer-0 input)
+    constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
+    constexpr int LDT = SR + CH;                // LDS row = one input column over SR rows (+pad)
     using C = TileCfg<NT, NT>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* AT = reinterpret_cast<T*>(smem);         // [H][LDT]
     const WgJob job = a.job[blockIdx.y];
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
     const int64_t r_end = r_begin + a.rows_per_chunk < a.RP ? r_begin + a.rows_per_chunk : a.RP;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
-    if (mt0 >= NT) return;
+    const bool active = mt0 < NT;
     const T* Z = reinterpret_cast<const T*>(a.dz8) + (int64_t)job.layer * a.RP * H;
     const T* X = reinterpret_cast<const T*>(a.act8) + job.act_off;
     const int col0 = job.kb * H;
+    const bool staged = a.gathered && job.layer == 0;
     bool kon[C::MTW];
 #pragma unroll
     for (int j = 0; j < C::MTW; ++j) kon[j] = col0 + (mt0 + j) * 16 < job.kp;
@@ -606,33 +764,96 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     float bsum[C::NTW];
 #pragma unroll
     for (int i = 0; i < C::NTW; ++i) bsum[i] = 0.f;
-    const bool do_bias = job.b_off >= 0 && wm == 0;
+    const bool do_bias = job.b_off >= 0 && wm == 0 && active;
     const typename Mf<T>::frag zero{};
+    auto bias_acc = [&](const typename Mf<T>::frag* fa) {
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i) {
+            if constexpr (VEC == 1) {
+                bsum[i] += to_f(fa[i]);
+            } else {
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) bsum[i] += (float)fa[i][v];
+            }
+        }
+    };
+    if (!staged) {
 #pragma unroll 2
-    for (int64_t m0 = r_begin; m0 < r_end; m0 += KSTEP) {
-        const int64_t mr = m0 + VEC * (lane >> 4);
-        typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
+        for (int64_t m0 = r_begin; m0 < r_end; m0 += KSTEP) {
+            if (!active) break;
+            const int64_t mr = m0 + VEC * (lane >> 4);
+            typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
 #pragma unroll
-        for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
 #pragma unroll
-        for (int j = 0; j < C::MTW; ++j)
-            fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
+            for (int j = 0; j < C::MTW; ++j)
+                fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
 #pragma unroll
-        for (int i = 0; i < C::NTW; ++i)
+            for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
-            for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
-        if (do_bias) {
+                for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
+            if (do_bias) bias_acc(fa);
+        }
+    } else {
+        // segment holding columns [col0, col0 + H) of the layer-0 input (segments are H wide)
+        int s = 0;
+        while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
+        const SrcSeg g = a.seg[s];
+        const T* src = reinterpret_cast<const T*>(g.p);
+        // consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the transposed
+        // LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots: conflict-free.
+        // Double buffered: the next stage's loads are in flight while this stage's MFMAs run.
+        constexpr int ITEMS = SR * (H / CH);
+        constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;  // 16-byte chunks per thread
+
+        u32x4 nxt[PER];
+        auto issue = [&](int64_t m0) {
 #pragma unroll
-            for (int i = 0; i < C::NTW; ++i) {
-                if constexpr (VEC == 1) {
-                    bsum[i] += to_f(fa[i]);
-                } else {
+            for (int q = 0; q < PER; ++q) {
+                const int it = threadIdx.x + q * MGN_THREADS;
+                const int r = it % SR, cc = (it / SR) * CH;
+                const int64_t row = m0 + r;
+                nxt[q] = u32x4{0u, 0u, 0u, 0u};
+                if (it < ITEMS && m0 < r_end && row < a.M) {
+                    const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
+                    nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + (col0 - g.coff) + cc);
+                }
+            }
+        };
+        issue(r_begin);
+        for (int64_t m0 = r_begin; m0 < r_end; m0 += SR) {
+            T* buf = AT + (size_t)((m0 - r_begin) / SR & 1) * H * LDT;
 #pragma unroll
-                    for (int v = 0; v < VEC; ++v) bsum[i] += (float)fa[i][v];
+            for (int q = 0; q < PER; ++q) {
+                const int it = threadIdx.x + q * MGN_THREADS;
+                if (it >= ITEMS) continue;
+                const int r = it % SR, cc = (it / SR) * CH;
+                const T* v = reinterpret_cast<const T*>(&nxt[q]);
+#pragma unroll
+                for (int e = 0; e < CH; ++e) buf[(size_t)(cc + e) * LDT + r] = v[e];
+            }
+            __syncthreads();
+            issue(m0 + SR);
+            if (active) {
+#pragma unroll
+                for (int ks = 0; ks < SR / KSTEP; ++ks) {
+                    const int64_t mr = m0 + ks * KSTEP + VEC * (lane >> 4);
+                    typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j)
+                        fb[j] = ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                        for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
+                    if (do_bias) bias_acc(fa);
                 }
             }
         }
     }
+    if (!active) return;
     float* part = a.part + (int64_t)blockIdx.x * a.G;
 #pragma unroll
     for (int i = 0; i < C::NTW; ++i)
@@ -813,13 +1034,18 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     a.out_ld = out_ld;
     a.resid = resid;
     a.act8 = sv->act;
-    for (int l = 0; l < m->n_layers; ++l) a.act_off[l] = act_off(*m, M, l);
+    for (int l = 0; l < m->n_layers; ++l) a.act_off[l] = act_off(*m, M, l, MODE != MODE_DENSE && !kSaveBlockInput);
     a.mask = reinterpret_cast<unsigned long long*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     a.z_save = sv->z;
     a.rden_save = sv->rden;
-    const size_t in_elems = (size_t)BM * (a.ldi > a.ldh ? a.ldi : a.ldh);
-    const size_t lds = (in_elems + (size_t)BM * a.ldh) * sizeof(T) + 4 * BM * sizeof(float);
+    a.ablate = ablate_mask();
+    size_t r0 = (size_t)BM * (a.ldi > a.ldh ? a.ldi : a.ldh) * sizeof(T);
+    const size_t zb = m->has_norm ? (size_t)BM * (H + 4) * sizeof(float) : 0;
+    if (zb > r0) r0 = zb;
+    r0 = (r0 + 15) / 16 * 16;
+    a.r0_elems = (int)(r0 / sizeof(T));
+    const size_t lds = r0 + (size_t)BM * a.ldh * sizeof(T) + 4 * BM * sizeof(float);
     auto fn = mlp_fwd_kernel<T, H, BM, MODE>;
     if (int e = set_lds((const void*)fn, lds)) return e;
     const int grid = (int)(rows_pad(M) / BM);
@@ -912,10 +1138,17 @@ int wgrad_rows_per_chunk(const mgn_mlp* m, int64_t M) {
 
 template <class T, int H>
 int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8, const float* dscale_part,
-                 int ntiles, float* part, float* grads, hipStream_t st) {
+                 int ntiles, float* part, float* grads, const MlpIn* gin, hipStream_t st) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
     a.RP = rows_pad(M);
+    a.M = M;
+    if (kSaveBlockInput) gin = nullptr;
+    a.gathered = gin != nullptr;
+    if (gin) {
+        for (int s2 = 0; s2 < gin->nseg; ++s2) a.seg[s2] = gin->seg[s2];
+        a.nseg = gin->nseg;
+    }
     a.H = H;
     a.rows_per_chunk = wgrad_rows_per_chunk(m, M);
     a.dz8 = dz8;
@@ -937,16 +1170,17 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8,
             j.kp = act_cols(*m, l);
             j.w_off = off;
             j.b_off = kb == 0 ? off + (int64_t)n * k : -1;
-            j.act_off = act_off(*m, M, l);
+            j.act_off = act_off(*m, M, l, gin != nullptr);
         }
         off += (int64_t)n * k + n;
     }
     a.njobs = nj;
     const int nchunks = (int)cdiv64(a.RP, a.rows_per_chunk);
     auto fn = mlp_wgrad_kernel<T, H>;
+    const size_t lds = gin ? 2 * (size_t)H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
     if (nchunks > 0) {
         ProfScope ps(PROF_WGRAD, st);
-        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), 0, st, a);
+        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
         MGN_LAUNCH_CHECK();
     }
     ProfScope ps2(PROF_WGRAD_REDUCE, st);
@@ -1019,12 +1253,12 @@ static int mlp_bwd_any(const mgn_mlp* m, int mode, int64_t M, const mgn_mlp_save
 }
 
 static int mlp_wgrad_any(const mgn_mlp* m, int64_t M, const void* act, const void* dz, const float* dsp,
-                         int ntiles, float* part, float* grads, hipStream_t st) {
+                         int ntiles, float* part, float* grads, const MlpIn* gin, hipStream_t st) {
     int rc = 0;
     if (m->dtype == MGN_F32) {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, act, dz, dsp, ntiles, part, grads, st)))
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, act, dz, dsp, ntiles, part, grads, gin, st)))
     } else {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, act, dz, dsp, ntiles, part, grads, st)))
+        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, act, dz, dsp, ntiles, part, grads, gin, st)))
     }
     return rc;
 }
@@ -1048,8 +1282,7 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
         return 0;
     }
     if (int e = mlp_bwd_any(m, mode, M, sv, dout, dout_dtype, dout_ld, o, dz, dsp, st)) return e;
-    (void)in;
-    return mlp_wgrad_any(m, M, sv->act, dz, dsp, ntiles, part, grads, st);
+    return mlp_wgrad_any(m, M, sv->act, dz, dsp, ntiles, part, grads, mode == MODE_DENSE ? nullptr : &in, st);
 }
 
 // =========================================================================== node combine
@@ -1066,17 +1299,40 @@ __global__ __launch_bounds__(MGN_THREADS) void node_combine_kernel(const T* __re
     const int64_t n = gid / LPN;
     const int c = (int)(gid % LPN) * CH;
     if (n >= N) return;
-    float acc[CH], t[CH];
+    float acc[CH], t[4][CH];
     Chunk<T>::load(dx_part + n * H + c, acc);
-    for (int k = col_ptr[n]; k < col_ptr[n + 1]; ++k) {
-        Chunk<T>::load(dxij + (int64_t)k * 2 * H + c, t);
+    const int kb = col_ptr[n], ke = col_ptr[n + 1];
+    int k = kb;
+    for (; k + 4 <= ke; k += 4) {
 #pragma unroll
-        for (int v = 0; v < CH; ++v) acc[v] += t[v];
+        for (int u = 0; u < 4; ++u) Chunk<T>::load(dxij + (int64_t)(k + u) * 2 * H + c, t[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < CH; ++v) acc[v] += t[u][v];
     }
-    for (int j = row_ptr[n]; j < row_ptr[n + 1]; ++j) {
-        Chunk<T>::load(dxij + (int64_t)row_perm[j] * 2 * H + H + c, t);
+    for (; k < ke; ++k) {
+        Chunk<T>::load(dxij + (int64_t)k * 2 * H + c, t[0]);
 #pragma unroll
-        for (int v = 0; v < CH; ++v) acc[v] += t[v];
+        for (int v = 0; v < CH; ++v) acc[v] += t[0][v];
+    }
+    const int jb = row_ptr[n], je = row_ptr[n + 1];
+    int j = jb;
+    for (; j + 4 <= je; j += 4) {
+        int e4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e4[u] = row_perm[j + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Chunk<T>::load(dxij + (int64_t)e4[u] * 2 * H + H + c, t[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < CH; ++v) acc[v] += t[u][v];
+    }
+    for (; j < je; ++j) {
+        Chunk<T>::load(dxij + (int64_t)row_perm[j] * 2 * H + H + c, t[0]);
+#pragma unroll
+        for (int v = 0; v < CH; ++v) acc[v] += t[0][v];
     }
     Chunk<T>::store(dx + n * H + c, acc);
 }
@@ -1126,8 +1382,9 @@ int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t 
 
 size_t mgn_mlp_backward_workspace_bytes(const mgn_mlp* m, int64_t rows) { return mlp_bwd_ws(m, rows); }
 
-int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int64_t* act_elems, int64_t* mask_words) {
-    *act_elems = act_off(*m, rows, m->n_layers);
+int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int32_t block_mlp, int64_t* act_elems,
+                        int64_t* mask_words) {
+    *act_elems = act_off(*m, rows, m->n_layers, block_mlp && !kSaveBlockInput);
     *mask_words = (int64_t)(m->n_layers - 1) * mask_words_per_layer(*m, rows);
     return 0;
 }

@@ -211,9 +211,10 @@ def _empty(n, dtype, device):
     return torch.empty(max(int(n), 1), dtype=dtype, device=device)
 
 
-def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z):
+def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
     ae, mw = ctypes.c_int64(), ctypes.c_int64()
-    nat.check(nat.lib().mgn_mlp_saved_elems(ctypes.byref(desc), rows, ctypes.byref(ae), ctypes.byref(mw)))
+    nat.check(nat.lib().mgn_mlp_saved_elems(ctypes.byref(desc), rows, int(block_mlp), ctypes.byref(ae),
+                                            ctypes.byref(mw)))
     act = _empty(ae.value, tdt, device)
     mask = _empty(mw.value, torch.int64, device)
     z = _empty(rows * spec.hidden, tdt, device) if need_z else None
@@ -224,8 +225,8 @@ def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z):
 
 
 def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device):
-    se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True)
-    sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None)
+    se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True, True)
+    sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None, True)
     aggr = _empty(topo.num_nodes * espec.hidden, tdt, device)
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
 

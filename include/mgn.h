@@ -90,7 +90,7 @@ typedef struct mgn_mlp {
 } mgn_mlp;
 
 /* Forward state kept for the backward. `act` holds the INPUT of every Linear (layer 0: the
- * gathered/concatenated MLP input; layer l>0: the ReLU output of layer l-1) in the row-octet
+ * MLP input — not for GraphNetBlock MLPs; layer l>0: the ReLU output of layer l-1) in the row-octet
  * layout (element (m,c) at ((m/8)*cols + c)*8 + m%8, rows padded to 64) that makes every weight-
  * gradient MFMA fragment one 16-byte load; `mask` holds the hidden layers' ReLU masks as 64-bit
  * wave-ballot words. Sizes: mgn_mlp_saved_elems(). */
@@ -100,7 +100,10 @@ typedef struct mgn_mlp_saved {
     void* z;      /* [M, hidden] last Linear output before RMSNorm (dtype); NULL w/o norm    */
     float* rden;  /* [M] RMSNorm denominator rms+eps; NULL w/o norm                          */
 } mgn_mlp_saved;
-int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int64_t* act_elems, int64_t* mask_words);
+/* block_mlp != 0 for the edge/node MLPs of a GraphNetBlock: their layer-0 input is not saved (the
+ * weight-gradient kernel re-gathers [e ‖ x_i ‖ x_j] / [x ‖ aggr]). */
+int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int32_t block_mlp, int64_t* act_elems,
+                        int64_t* mask_words);
 
 /* Pack job: one nn.Linear weight [n, k] fp32 row-major → fragment buffers (dtype). */
 typedef struct mgn_pack_job {
