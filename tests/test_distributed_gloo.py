@@ -1,0 +1,106 @@
+"""Graph-sharded data parallelism on CPU (gloo, world_size 2): two ranks holding half of a batch
+each must reproduce the single-process step on the whole batch — normaliser statistics, loss and
+SUM-all-reduced gradients (graphphysics/training/distributed.py). The model compute
+here is the oracle (CPU); the exchange logic is the product's."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _OracleModel(torch.nn.Module):
+    K = 0
+
+    def __init__(self):
+        super().__init__()
+        from oracle import mgn_oracle as O
+
+        torch.manual_seed(0)
+        self.epd = O.OracleEPD(2, 11, 3, 2, 16)
+
+    def forward(self, graph):
+        return self.epd(graph.x, graph.edge_index, graph.edge_attr)
+
+
+def _shard(b, rank, world):
+    n, g = b["nodes_per_graph"], b["num_graphs"] // world
+    lo, hi = rank * g * n, (rank + 1) * g * n
+    ei = b["edge_index"]
+    keep = (ei[0] >= lo) & (ei[0] < hi)
+    return {"x": b["x"][lo:hi], "y": b["y"][lo:hi], "edge_index": ei[:, keep] - lo,
+            "edge_attr": b["edge_attr"][keep]}
+
+
+def _step(sim, d, group):
+    from graphphysics.training.distributed import allreduce_gradients, global_masked_mse
+    from graphphysics.utils.data import Data
+    from graphphysics.utils.loss import masked_mse
+    from graphphysics.utils.nodetype import NodeType
+
+    data = Data(**{k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in d.items()})
+    net, tdn, _ = sim(data)
+    masks = [NodeType.NORMAL, NodeType.OUTFLOW]
+    loss = (global_masked_mse(tdn, net, data.x[:, 2], masks, group) if group is not None
+            else masked_mse(tdn, net, data.x[:, 2], masks))
+    loss.backward()
+    if group is not None:
+        allreduce_gradients(sim.parameters(), group)
+    return loss
+
+
+def _worker(rank, world, port, out):
+    import sys
+
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "graph-physics_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+
+    torch.set_num_threads(1)
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    sim.set_process_group(dist.group.WORLD)
+    loss = _step(sim, _shard(b, rank, world), dist.group.WORLD)
+    dist.all_reduce(loss.detach())
+    res = {"loss": loss.item(), "acc": sim._node_normalizer._acc_sum.clone(),
+           "cnt": sim._edge_normalizer._acc_count.item(),
+           "grads": [p.grad.clone() for p in sim.parameters()]}
+    torch.save(res, os.path.join(out, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_two_rank_step_equals_single_process_step():
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+
+    port = 29500 + os.getpid() % 1000
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(2)]
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    loss = _step(sim, {k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}, None)
+    assert abs(r[0]["loss"] - loss.item()) <= 1e-6 * abs(loss.item())
+    assert r[0]["cnt"] == r[1]["cnt"] == b["edge_index"].shape[1]
+    torch.testing.assert_close(r[0]["acc"], sim._node_normalizer._acc_sum, rtol=1e-5, atol=1e-5)
+    for g0, g1, p in zip(r[0]["grads"], r[1]["grads"], sim.parameters()):
+        assert torch.equal(g0, g1)  # identical on every rank after the all-reduce
+        torch.testing.assert_close(g0, p.grad, rtol=2e-4, atol=1e-6)
+
+
+def test_flat_grad_buffer_detection():
+    from graphphysics.training.distributed import flat_grad_buffer
+
+    flat = torch.arange(10.0)
+    a, b = torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(6))
+    a.grad, b.grad = flat[:4], flat[4:]
+    f = flat_grad_buffer([a, b])
+    assert f is not None and f.numel() == 10 and f.data_ptr() == flat.data_ptr()
+    b.grad = torch.zeros(6)
+    assert flat_grad_buffer([a, b]) is None

@@ -1,0 +1,177 @@
+"""Host-side logic of the drop-in package, on CPU (no kernels): module structure / state_dict
+compatibility with the reference, RNG-order parity of initialisation, flat parameter storage,
+normaliser / loss / scheduler semantics against the oracle and golden vectors, mesh construction."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _golden(name):
+    z = np.load(os.path.join(G, name))
+    return {k: z[k] for k in z.files}
+
+
+def test_epd_state_dict_keys_and_init_match_reference():
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    z = _golden("cylinder_golden.npz")
+    for tag, mp, h in (("cfgA_init", 5, 32), ("cfgB_init", 15, 128)):
+        torch.manual_seed(0)
+        m = EncodeProcessDecode(mp, 11, 3, 2, h)
+        sd = m.state_dict()
+        pre = tag + "::model."
+        ref_keys = sorted(k[len(pre):] for k in z if k.startswith(pre))
+        assert sorted(sd) == ref_keys
+        for k, v in sd.items():
+            assert v.double().sum().item() == float(z[f"{tag}::model.{k}"]), k
+    assert (m.K, m.d, m.temperature, m.hidden_size, m.only_processor) == (0, 2, None, 128, False)
+
+
+def test_golden_weights_load_into_drop_in_modules():
+    from graphphysics.models.layers import GraphNetBlock
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    z = _golden("block_cycle_h16.npz")
+    GraphNetBlock(16).load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w::")})
+    z = _golden("epd_random_h16.npz")
+    EncodeProcessDecode(3, 8, 4, 3, 16).load_state_dict(
+        {k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w::")})
+
+
+def test_flat_parameters_and_plan_order():
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    m = EncodeProcessDecode(3, 11, 3, 2, 32)
+    flat = m._flat_params
+    o = 0
+    for p in m.parameters():
+        assert p.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
+        assert p.storage_offset() == o
+        o += p.numel()
+    assert o == flat.numel()
+    m = m.double().float()  # _apply re-homes parameters into a fresh flat buffer
+    assert all(p.untyped_storage().data_ptr() == m._flat_params.untyped_storage().data_ptr()
+               for p in m.parameters())
+    plan = m._get_plan()
+    assert [s.in_dim for s in plan.specs[:3]] == [11, 3, 32]
+    assert [s.out_dim for s in plan.specs[:3]] == [32, 32, 2]
+    assert plan.specs[2].norm is None and plan.specs[3].norm is not None
+    assert plan.offsets[1] == plan.specs[0].numel
+    assert plan.numel == sum(p.numel() for p in m.parameters())
+    g = torch.arange(plan.numel, dtype=torch.float32)
+    views = plan.grad_views(g)
+    assert [v.shape for v in views] == [p.shape for p in m.parameters()]
+    with pytest.raises(ValueError):
+        _engine.MlpSpec(torch.nn.Sequential(torch.nn.Linear(3, 4), torch.nn.Tanh(), torch.nn.Linear(4, 4)))
+
+
+def test_gmm_heads_are_rejected_loudly():
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    with pytest.raises(NotImplementedError):
+        EncodeProcessDecode(2, 11, 3, 2, 16, num_mixture_components=2, temperature=1.0)
+
+
+def test_normalizer_matches_reference_semantics():
+    from graphphysics.models.layers import Normalizer
+
+    g = torch.Generator().manual_seed(0)
+    mine = Normalizer(5, max_accumulations=3, device="cpu")
+    ref = O.OracleNormalizer(5, max_accumulations=3)
+    for i in range(5):  # crosses max_accumulations: accumulation must stop
+        d = torch.randn(17 + i, 5, generator=g) * 3 + 1
+        a, b = mine(d, True), ref(d, True)
+        assert torch.equal(a, b)
+    assert torch.equal(mine.inverse(a), ref.inverse(a))
+    assert mine._num_accumulations.item() == 3
+    assert torch.equal(mine._acc_sum, ref.acc_sum)
+    e = torch.randn(4, 5, generator=g)
+    assert torch.equal(mine(e, False), ref(e, False))
+
+
+class _ZeroModel(torch.nn.Module):
+    K = 0
+
+    def forward(self, graph):
+        return torch.zeros(graph.x.shape[0], 2) + graph.x[:, :2].sum() * 0
+
+
+def test_simulator_preamble_matches_reference():
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(2)
+    x, y = torch.from_numpy(b["x"]), torch.from_numpy(b["y"])
+    ei, ea = torch.from_numpy(b["edge_index"]), torch.from_numpy(b["edge_attr"])
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _ZeroModel(), "cpu")
+    ref = O.OracleSimulator(lambda xn, e_, ean: torch.zeros(xn.shape[0], 2), 11, 3, 2)
+    for _ in range(2):
+        _, tdn, _ = sim(Data(x=x, y=y, edge_index=ei, edge_attr=ea))
+        _, tdn_r, _ = ref.forward(x, y, ei, ea, True)
+        assert torch.equal(tdn, tdn_r)
+    assert torch.equal(sim._node_normalizer._acc_sum, ref.node_norm.acc_sum)
+    assert torch.equal(sim._edge_normalizer._acc_sum_squared, ref.edge_norm.acc_sum_squared)
+    sim.eval()
+    _, _, out = sim(Data(x=x, y=y, edge_index=ei, edge_attr=ea))
+    _, _, out_r = ref.forward(x, y, ei, ea, False)
+    assert torch.equal(out, out_r)
+
+
+def test_losses():
+    from graphphysics.utils.loss import L2Loss, masked_mse
+    from graphphysics.utils.nodetype import NodeType
+
+    g = torch.Generator().manual_seed(0)
+    t, o = torch.randn(100, 2, generator=g), torch.randn(100, 2, generator=g)
+    nt = torch.randint(0, 7, (100,), generator=g).float()
+    masks = [NodeType.NORMAL, NodeType.OUTFLOW]
+    ref = O.l2_loss(t, o, nt)
+    assert torch.equal(L2Loss()(t, o, nt, masks), ref)
+    torch.testing.assert_close(masked_mse(t, o, nt, masks), ref, rtol=1e-6, atol=0)
+
+
+def test_scheduler_matches_golden():
+    from graphphysics.utils.scheduler import CosineWarmupScheduler
+
+    z = _golden("cylinder_golden.npz")
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p], lr=1e-3)
+    sch = CosineWarmupScheduler(opt, warmup=5, max_iters=100)
+    lrs = []
+    for _ in range(3):
+        opt.step()
+        sch.step()
+        lrs.append(opt.param_groups[0]["lr"])
+    np.testing.assert_array_equal(np.array(lrs), z["cfgA/lrs"])
+
+
+def test_mesh_construction_pins():
+    from graphphysics.utils import meshes
+
+    m = meshes.load_cylinder_mesh()
+    n = m["pos"].shape[0]
+    ei = meshes.triangles_to_edge_index(m["triangles"], n)
+    assert ei.shape == (2, 11070)
+    # k-hop=2 count pinned by reference tests/graphphysics/dataset/test_xdmfdataset.py:228-230
+    assert meshes.khop_edge_index(ei, n, 2).shape == (2, 32638)
+    b = meshes.cylinder_batch(8)
+    assert b["x"].shape == (15384, 3) and b["edge_index"].shape == (2, 88560)
+    assert (np.diff(b["edge_index"][0]) >= 0).all()  # batching keeps (row, col) order
+
+
+def test_product_path_refuses_cpu_tensors():
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    m = EncodeProcessDecode(1, 5, 3, 2, 16)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(Data(x=torch.zeros(4, 5), edge_index=torch.zeros((2, 1), dtype=torch.long),
+               edge_attr=torch.zeros(1, 3)))
