@@ -157,6 +157,8 @@ def main():
         step_flops = 3 * (a.mp * (fe + fn) + 2 * (3 * h + 3 * h * h) * E + 2 * (11 * h + 3 * h * h) * N
                           + 2 * (3 * h * h + h * 2) * N)
         roof["step_tflops_per_s"] = round(step_flops * a.steps / dt / 1e12, 2)
+    if roof is not None:
+        roof["traffic"], roof["traffic_note"] = pmc_traffic(roof["kernel"])
     value = world * a.steps / dt
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
@@ -181,6 +183,23 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch of `kernel_class` from the committed rocprofv3 PMC passes
+    (profiles/<round>_traffic.json, made by tools/profile_round.sh + tools/pmc_traffic.py), used only
+    when they were measured on the same kernel sources (sha256 stamp)."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import sources_sha
+
+    sha = sources_sha()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("sources_sha") == sha and kernel_class in d.get("kernels", {}):
+            return round(d["kernels"][kernel_class]["hbm_bytes"]), os.path.relpath(f, ROOT)
+    return None, "no PMC traffic measured for these kernel sources (run tools/profile_round.sh)"
 
 
 def one_step_mse(sim, mesh, dev, a):

@@ -1,0 +1,69 @@
+"""Parse rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-kernel-class HBM bytes per launch.
+
+Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): counters are in KB (x1024);
+on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads -> doubled.
+WRITE_SIZE is exact for 16-B stores. Output is stamped with the sha256 of the kernel sources so
+bench.py only reports traffic measured on the same build.
+    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import re
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def sources_sha():
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "graph-physics_amd", "csrc", "*"))) + [
+        os.path.join(ROOT, "include", "mgn.h")]
+    for f in files:
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def kernel_class(name):
+    m = re.search(r"mlp_(fwd|bwd)_kernel.*?Li(\d+)ELi(\d+)ELi(\d)E", name)
+    if m:
+        return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[m.group(4)]
+    for key, cls in (("mlp_wgrad_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
+                     ("node_combine_kernel", "combine"), ("adamw", "adamw"), ("pack_kernel", "pack")):
+        if key in name:
+            return cls
+    return None
+
+
+def load(path, counter):
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        c = kernel_class(r["Kernel_Name"])
+        if c:
+            per.setdefault((c, r["Kernel_Name"]), []).append(float(r["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main(fetch_csv, write_csv, out):
+    f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+    res = {}
+    for key in f:
+        cls, name = key
+        fb = 2.0 * statistics.median(f[key])
+        wb = statistics.median(w.get(key, [0.0]))
+        if cls in res and "bf16" not in name and "DF16b" not in name:
+            continue  # prefer the bf16 (bench) instantiation
+        res[cls] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb, "launches": len(f[key]),
+                    "kernel": name}
+    json.dump({"sources_sha": sources_sha(), "fetch_correction": 2.0, "unit": "bytes per launch (median)",
+               "kernels": res}, open(out, "w"), indent=1)
+    print(json.dumps({k: round(v["hbm_bytes"] / 1e6, 1) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
