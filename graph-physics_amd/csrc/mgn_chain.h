@@ -1,0 +1,54 @@
+// Internal interface of the register-chained bf16 h=128 edge-MLP kernels (mgn_chain.hip).
+#pragma once
+#include "mgn_common.h"
+
+struct ChainFwdArgs {
+    const __bf16* e;            // [M][128] edge state, target-sorted
+    const float* proj;          // [N][256] node projections (x·W0bᵀ ‖ x·W0cᵀ)
+    const int32_t* proj_i;      // dst per edge
+    const int32_t* proj_j;      // src per edge
+    const __bf16* wpack;        // forward 16x16x32 fragments of the 4 layers
+    int64_t woff[4];
+    int32_t wks[4];
+    const float* bias[4];
+    const float* scale;
+    float dinv;
+    int64_t M, ntiles;
+    __bf16* out;                // [M][128] e + MLP(...)
+    __bf16* z_save;             // [M][128] pre-norm output
+    float* rden_save;           // [M]
+    __bf16* act8;               // R8 saved inputs of layers 1..3
+    int64_t act_off[4];
+    unsigned long long* mask;   // [3][ntiles*64]: lane-owned ReLU bits
+    int64_t mask_stride;
+};
+
+struct ChainBwdArgs {
+    const __bf16* dout;         // [M][128] de_out
+    const __bf16* gath;         // [N][128] d_aggr, added at gath_idx[row]
+    const int32_t* gath_idx;
+    const __bf16* z_save;
+    const float* rden_save;
+    const float* scale;
+    float dinv;
+    const unsigned long long* mask;
+    int64_t mask_stride;
+    const __bf16* wtpack;       // transposed 16x16x32 fragments of the 4 layers
+    int64_t woff[4];
+    int32_t wks[4];
+    int64_t M, ntiles;
+    __bf16* dz8;                // R8 [4][RP][128]
+    int64_t RP;
+    float* dscale_part;         // [grid][128]
+    __bf16* de;                 // [M][128] de_out + dZ0·W0a
+    __bf16* dz0;                // [M][128] dZ0 row-major
+};
+
+bool chain_eligible(const mgn_mlp* m);
+int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
+                       int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
+// nparts: number of dscale partial rows written (the reduction's row count)
+int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
+                        const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
+                        hipStream_t st);
+size_t chain_lds_bytes();

@@ -18,15 +18,12 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "mgn_chain.h"
 #include "mgn_common.h"
 
 namespace {
 
 enum { MODE_DENSE = 0, MODE_EDGE = 1, MODE_NODE = 2 };
-
-// Block MLPs: save the layer-0 input in R8 (true) or re-gather it in the weight-gradient kernel
-// through an LDS transpose (false: 136 MB less HBM traffic per edge block).
-constexpr bool kSaveBlockInput = false;
 
 template <int NT, int MT>
 struct TileCfg {
@@ -46,19 +43,25 @@ struct Gemm {
     int nt0, mt0;
     bool active;
 
-    __device__ __forceinline__ void run(const T* __restrict__ wp, int KS, const T* lds, int ldl, bool skip = false) {
+    // KS k-steps; fragment (n-tile t, k-step s) at wp + (t*kstride + s) fragments (kstride >= KS
+    // lets a GEMM use a column block of a wider packed weight). accumulate: keep acc.
+    __device__ __forceinline__ void run(const T* __restrict__ wp, int KS, const T* lds, int ldl, bool skip = false,
+                                        int kstride = 0, bool accumulate = false) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         const int wn = wave % C::WN, wm = wave / C::WN;
         nt0 = wn * C::NTW;
         mt0 = wm * C::MTW;
         active = mt0 < MT;
+        if (!accumulate) {
 #pragma unroll
-        for (int i = 0; i < C::NTW; ++i)
+            for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
-            for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        }
         if (!active || skip) return;
+        if (kstride <= 0) kstride = KS;
         const T* bp = lds + (size_t)(mt0 * 16 + (lane & 15)) * ldl + VEC * (lane >> 4);
-        const T* ap = wp + ((size_t)nt0 * KS * 64 + lane) * VEC;
+        const T* ap = wp + ((size_t)nt0 * kstride * 64 + lane) * VEC;
         // weight fragments come from L2: keep PD k-steps of them in flight (register ring with
         // compile-time slots; the k loop is unrolled by PD so every ring index is static)
         constexpr int PD = 4;
@@ -67,7 +70,7 @@ struct Gemm {
         for (int u = 0; u < PD; ++u)
 #pragma unroll
             for (int i = 0; i < C::NTW; ++i)
-                if (u < KS) ring[u][i] = ld_frag(ap + ((size_t)i * KS + u) * 64 * VEC);
+                if (u < KS) ring[u][i] = ld_frag(ap + ((size_t)i * kstride + u) * 64 * VEC);
         for (int k0 = 0; k0 < KS; k0 += PD) {
 #pragma unroll
             for (int u = 0; u < PD; ++u) {
@@ -78,7 +81,7 @@ struct Gemm {
                 for (int i = 0; i < C::NTW; ++i) a[i] = ring[u][i];
                 if (ks + PD < KS) {
 #pragma unroll
-                    for (int i = 0; i < C::NTW; ++i) ring[u][i] = ld_frag(ap + ((size_t)i * KS + ks + PD) * 64 * VEC);
+                    for (int i = 0; i < C::NTW; ++i) ring[u][i] = ld_frag(ap + ((size_t)i * kstride + ks + PD) * 64 * VEC);
                 }
 #pragma unroll
                 for (int j = 0; j < C::MTW; ++j) b[j] = ld_frag(bp + (size_t)j * 16 * ldl + ks * KSTEP);
@@ -210,8 +213,13 @@ struct FwdArgs {
     SrcSeg seg[3];
     int32_t nseg;
     int32_t L, K0, H, NOUT, has_norm, ldi, ldh;
+    int32_t Kpack0, kstride0;  // layer-0 packed width (K0 < Kpack0: EDGE uses the e-column block)
     int64_t M;
     const void* wpack;
+    // EDGE: node projections P [N][2H] fp32 (x·W0bᵀ ‖ x·W0cᵀ), added at rows proj_i/proj_j
+    const float* proj;
+    const int32_t* proj_i;
+    const int32_t* proj_j;
     const float* bias[MGN_MAX_LAYERS];
     const float* scale;
     float dinv;
@@ -410,15 +418,15 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     }
     __syncthreads();
     // the layer-0 input of edge/node MLPs is re-gathered by the weight-gradient kernel
-    if ((MODE == MODE_DENSE || kSaveBlockInput) && !(a.ablate & 2))
+    if (MODE == MODE_DENSE && !(a.ablate & 2))
         copy_out_r8<T, BM>(In, a.ldi, KP0, reinterpret_cast<T*>(a.act8) + a.act_off[0], row0);
 
     const T* wp = reinterpret_cast<const T*>(a.wpack);
     const T* cur = In;
-    int ldc = a.ldi, KS = KP0 / KSTEP, K = a.K0;
+    int ldc = a.ldi, KS = KP0 / KSTEP, K = a.Kpack0;
     for (int l = 0; l < a.L - 1; ++l) {
         Gemm<T, NTH, MT> g;
-        g.run(wp, KS, cur, ldc, a.ablate & 4);
+        g.run(wp, KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
         T* nxt = (l & 1) ? P1 : P0;
         if (g.active) {
             const float* b = a.bias[l];
@@ -429,9 +437,16 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                 for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
                     const int m = g.m_of(j);
+                    f4 pp = {0.f, 0.f, 0.f, 0.f};
+                    if (MODE == MODE_EDGE && l == 0 && row0 + m < a.M) {
+                        // [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]
+                        const f4 pi = *reinterpret_cast<const f4*>(a.proj + (int64_t)a.proj_i[row0 + m] * (2 * H) + n);
+                        const f4 pj = *reinterpret_cast<const f4*>(a.proj + (int64_t)a.proj_j[row0 + m] * (2 * H) + H + n);
+                        pp = pi + pj;
+                    }
                     f4 v;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(g.acc[i][j][r] + bb[r], 0.f);
+                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(g.acc[i][j][r] + bb[r] + pp[r], 0.f);
                     st4(nxt + (size_t)m * a.ldh + n, v);
                     const int64_t mtile = (row0 >> 4) + g.mt0 + j;
                     unsigned long long* mw = a.mask + (int64_t)l * a.mask_stride + (mtile * NTH + g.nt0 + i) * 4;
@@ -473,6 +488,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
 struct BwdArgs {
     int64_t M;
     int32_t L, K0, H, NOUT, has_norm, ldh, mode;
+    int32_t Kpack0;         // layer-0 packed width (EDGE: 3H, of which the e block K0 = H is used)
     float dinv;
     const void* wtpack;
     const float* scale;
@@ -492,7 +508,7 @@ struct BwdArgs {
     int32_t din_dtype;
     int64_t din_ld;
     void* o1;               // EDGE: de_in [M][H]; NODE: dx_part [M][H]  (T)
-    void* o2;               // EDGE: dxij [M][2H]; NODE: d_aggr [M][H]   (T)
+    void* o2;               // EDGE: dZ_0 [M][H] row-major; NODE: d_aggr [M][H]   (T)
 };
 
 template <class T, int H, int BM, int MODE>
@@ -608,7 +624,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         int64_t o = 0;
         for (int l = 0; l < a.L; ++l) {
             off[l] = o;
-            const int n = l == a.L - 1 ? NO : H, k = l == 0 ? a.K0 : H;
+            const int n = l == a.L - 1 ? NO : H, k = l == 0 ? a.Kpack0 : H;
             o += linear_pack_elems(n, k, dtype_id<T>());
         }
     }
@@ -651,6 +667,17 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 
     // ---- layer 0 : dA0 = dZ_0 · W_0, K0 columns in chunks of H
     if (MODE == MODE_DENSE && a.din == nullptr) return;
+    if (MODE == MODE_EDGE) {
+        // dZ_0 row-major for the node side: d(x·W0bᵀ)[v] = Σ_{dst(k)=v} dZ_0[k], likewise src
+        constexpr int CH = 16 / sizeof(T);
+        for (int it = tid; it < BM * (H / CH); it += MGN_THREADS) {
+            const int r = it / (H / CH), cc = (it - r * (H / CH)) * CH;
+            const int64_t row = row0 + r;
+            if (row < a.M)
+                *reinterpret_cast<u32x4*>(reinterpret_cast<T*>(a.o2) + row * H + cc) =
+                    *reinterpret_cast<const u32x4*>(cur + (size_t)r * a.ldh + cc);
+        }
+    }
     const int KS0 = cdiv(a.L == 1 ? NO : H, KSTEP);
     const int nchunk = cdiv(cdiv(a.K0, 16), NTH);
     for (int c = 0; c < nchunk; ++c) {
@@ -679,9 +706,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
                     for (int e = 0; e < CH; ++e) v[e] = d[e] + v[e];
                     Chunk<T>::store(reinterpret_cast<T*>(a.o1) + row * H + cc, v);
-                } else if (MODE == MODE_EDGE) {
-                    Chunk<T>::store(reinterpret_cast<T*>(a.o2) + row * (2 * H) + (c - 1) * H + cc, v);
-                } else {
+                } else if (MODE == MODE_NODE) {
                     Chunk<T>::store(reinterpret_cast<T*>(a.o2) + row * H + cc, v);
                 }
             }
@@ -718,8 +743,9 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 // (layer, 128-column block) output tile over a chunk of rows; partial tiles go to fp32 slabs that
 // wgrad_reduce sums in a fixed order (deterministic, no atomics).
 struct WgJob {
-    int32_t layer, kb, n, k, kp, pad;
-    int64_t w_off, b_off, act_off;  // b_off < 0: no bias for this job
+    int32_t layer, kb, n, k, kp, staged;  // staged: B operand re-gathered from seg[] through LDS
+    int64_t w_off, b_off, act_off;        // b_off < 0: no bias for this job
+    int32_t zl, pad;                      // dZ operand = R8 block zl of dz8
 };
 struct WgArgs {
     int64_t RP, M;
@@ -749,10 +775,10 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
     const bool active = mt0 < NT;
-    const T* Z = reinterpret_cast<const T*>(a.dz8) + (int64_t)job.layer * a.RP * H;
+    const T* Z = reinterpret_cast<const T*>(a.dz8) + (int64_t)job.zl * a.RP * H;
     const T* X = reinterpret_cast<const T*>(a.act8) + job.act_off;
     const int col0 = job.kb * H;
-    const bool staged = a.gathered && job.layer == 0;
+    const bool staged = job.staged != 0;
     bool kon[C::MTW];
 #pragma unroll
     for (int j = 0; j < C::MTW; ++j) kon[j] = col0 + (mt0 + j) * 16 < job.kp;
@@ -999,6 +1025,10 @@ int check_mlp(const mgn_mlp* m) {
 struct MlpIn {
     SrcSeg seg[3];
     int nseg;
+    int K0;               // staged layer-0 columns (0: m->in_dim)
+    const float* proj;    // EDGE: node projections (see FwdArgs)
+    const int32_t* proj_i;
+    const int32_t* proj_j;
 };
 
 template <class T, int H, int MODE>
@@ -1011,11 +1041,16 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     for (int s = 0; s < in.nseg; ++s) a.seg[s] = in.seg[s];
     a.nseg = in.nseg;
     a.L = m->n_layers;
-    a.K0 = m->in_dim;
+    a.K0 = in.K0 ? in.K0 : m->in_dim;
+    a.Kpack0 = m->in_dim;
+    a.kstride0 = cdiv(m->in_dim, Mf<T>::KSTEP);
+    a.proj = in.proj;
+    a.proj_i = in.proj_i;
+    a.proj_j = in.proj_j;
     a.H = H;
     a.NOUT = m->out_dim;
     a.has_norm = m->has_norm;
-    a.ldi = pad_ld<T>(rup(m->in_dim, Mf<T>::KSTEP));
+    a.ldi = pad_ld<T>(rup(a.K0, Mf<T>::KSTEP));
     a.ldh = pad_ld<T>(rup(H, Mf<T>::KSTEP));
     a.M = M;
     a.wpack = m->wpack;
@@ -1034,7 +1069,7 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     a.out_ld = out_ld;
     a.resid = resid;
     a.act8 = sv->act;
-    for (int l = 0; l < m->n_layers; ++l) a.act_off[l] = act_off(*m, M, l, MODE != MODE_DENSE && !kSaveBlockInput);
+    for (int l = 0; l < m->n_layers; ++l) a.act_off[l] = act_off(*m, M, l, MODE != MODE_DENSE);
     a.mask = reinterpret_cast<unsigned long long*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     a.z_save = sv->z;
@@ -1075,7 +1110,8 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     memset(&a, 0, sizeof(a));
     a.M = M;
     a.L = m->n_layers;
-    a.K0 = m->in_dim;
+    a.K0 = MODE == MODE_EDGE ? H : m->in_dim;
+    a.Kpack0 = m->in_dim;
     a.H = H;
     a.NOUT = m->out_dim;
     a.has_norm = m->has_norm;
@@ -1123,34 +1159,64 @@ int64_t grad_G(const mgn_mlp* m) {
     return g;
 }
 
-int wgrad_jobs(const mgn_mlp* m) { return cdiv(m->in_dim, m->hidden) + (m->n_layers - 1); }
-
 // rows per chunk: enough workgroups to fill the chip (~512), at most 64 partial slabs
-int wgrad_rows_per_chunk(const mgn_mlp* m, int64_t M) {
-    const int64_t RP = rows_pad(M);
-    int64_t chunks = cdiv64(512, wgrad_jobs(m));
+int wgrad_rows_per_chunk(int64_t RP, int njobs) {
+    int64_t chunks = cdiv64(512, njobs);
     if (chunks > 64) chunks = 64;
     int64_t r = cdiv64(RP, chunks);
     r = cdiv64(r, 64) * 64;
     if (r < 64) r = 64;
     return (int)r;
 }
+// upper bound of the slab count over any job count (RP is a multiple of 64)
+int64_t wgrad_max_chunks(int64_t RP) {
+    int64_t c = RP / 64;
+    if (c > 64) c = 64;
+    return c < 1 ? 1 : c;
+}
+
+int launch_reduce(const mgn_mlp* m, const float* part, int nchunks, const float* dscale_part, int ntiles,
+                  float* grads, hipStream_t st) {
+    ProfScope ps(PROF_WGRAD_REDUCE, st);
+    const int64_t G = grad_G(m);
+    const int NS = m->has_norm ? m->out_dim : 0;
+    const unsigned blocks = (unsigned)(cdiv64(G, 64) + NS);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, part, nchunks, G, dscale_part,
+                       ntiles, NS, grads);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
 
 template <class T, int H>
+int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
+    a.njobs = nj;
+    auto fn = mlp_wgrad_kernel<T, H>;
+    const size_t lds = a.gathered ? 2 * (size_t)H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
+    if (nchunks > 0 && nj > 0) {
+        ProfScope ps(PROF_WGRAD, st);
+        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
+        MGN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+// Weight gradients of one MLP over M rows, then the slab reduction into grads. l0_jobs limits the
+// layer-0 column blocks (a block edge MLP covers only its e block here; see launch_wgrad_proj).
+// nchunks_out: the slab count used (the projection launch must write the same slabs).
+template <class T, int H>
 int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8, const float* dscale_part,
-                 int ntiles, float* part, float* grads, const MlpIn* gin, hipStream_t st) {
+                 int ntiles, float* part, float* grads, const MlpIn* gin, int l0_jobs, int* nchunks_out,
+                 bool reduce, hipStream_t st) {
     WgArgs a;
     memset(&a, 0, sizeof(a));
     a.RP = rows_pad(M);
     a.M = M;
-    if (kSaveBlockInput) gin = nullptr;
     a.gathered = gin != nullptr;
     if (gin) {
         for (int s2 = 0; s2 < gin->nseg; ++s2) a.seg[s2] = gin->seg[s2];
         a.nseg = gin->nseg;
     }
     a.H = H;
-    a.rows_per_chunk = wgrad_rows_per_chunk(m, M);
     a.dz8 = dz8;
     a.act8 = act8;
     a.part = part;
@@ -1160,7 +1226,9 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8,
     for (int l = 0; l < m->n_layers; ++l) {
         int n, k;
         mlp_layer_shape(*m, l, &n, &k);
-        for (int kb = 0; kb < cdiv(k, H); ++kb) {
+        int nkb = cdiv(k, H);
+        if (l == 0 && l0_jobs > 0 && l0_jobs < nkb) nkb = l0_jobs;
+        for (int kb = 0; kb < nkb; ++kb) {
             MGN_REQUIRE(nj < 12, "too many weight-gradient jobs");
             WgJob& j = a.job[nj++];
             j.layer = l;
@@ -1168,28 +1236,54 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8,
             j.n = n;
             j.k = k;
             j.kp = act_cols(*m, l);
+            j.staged = gin != nullptr && l == 0;
+            j.zl = l;
             j.w_off = off;
             j.b_off = kb == 0 ? off + (int64_t)n * k : -1;
             j.act_off = act_off(*m, M, l, gin != nullptr);
         }
         off += (int64_t)n * k + n;
     }
-    a.njobs = nj;
+    a.rows_per_chunk = wgrad_rows_per_chunk(a.RP, nj);
     const int nchunks = (int)cdiv64(a.RP, a.rows_per_chunk);
-    auto fn = mlp_wgrad_kernel<T, H>;
-    const size_t lds = gin ? 2 * (size_t)H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
-    if (nchunks > 0) {
-        ProfScope ps(PROF_WGRAD, st);
-        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
-        MGN_LAUNCH_CHECK();
+    if (nchunks_out) *nchunks_out = nchunks;
+    if (int e = launch_wgrad_kernel<T, H>(a, nj, nchunks, st)) return e;
+    return reduce ? launch_reduce(m, part, nchunks, dscale_part, ntiles, grads, st) : 0;
+}
+
+// dW0[:, H:2H] = Σ_v dP_i[v]ᵀ x[v] and dW0[:, 2H:3H] = Σ_v dP_j[v]ᵀ x[v] of a block edge MLP (the
+// node-side form of Σ_k dZ0[k]ᵀ x[dst(k)] / x[src(k)]), into the same nchunks slabs as the edge
+// rows (chunks past the node rows write zeros), so one reduction sums both.
+template <class T, int H>
+int launch_wgrad_proj(const mgn_mlp* m, int64_t N, const void* dP8, const void* x, float* part, int nchunks,
+                      hipStream_t st) {
+    WgArgs a;
+    memset(&a, 0, sizeof(a));
+    a.RP = rows_pad(N);
+    a.M = N;
+    a.gathered = 1;
+    a.seg[0] = SrcSeg{x, nullptr, H, H, dtype_id<T>(), H, 0};
+    a.seg[1] = SrcSeg{x, nullptr, H, H, dtype_id<T>(), 2 * H, 0};
+    a.nseg = 2;
+    a.H = H;
+    a.dz8 = dP8;
+    a.part = part;
+    a.G = grad_G(m);
+    for (int s2 = 0; s2 < 2; ++s2) {
+        WgJob& j = a.job[s2];
+        j.layer = 0;
+        j.kb = 1 + s2;
+        j.n = H;
+        j.k = m->in_dim;
+        j.kp = m->in_dim;
+        j.staged = 1;
+        j.zl = s2;
+        j.w_off = 0;
+        j.b_off = -1;
     }
-    ProfScope ps2(PROF_WGRAD_REDUCE, st);
-    const int NS = m->has_norm ? m->out_dim : 0;
-    const unsigned blocks = (unsigned)(cdiv64(a.G, 64) + NS);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, (const float*)part, nchunks,
-                       a.G, dscale_part, ntiles, NS, grads);
-    MGN_LAUNCH_CHECK();
-    return 0;
+    if (nchunks <= 0) return 0;
+    a.rows_per_chunk = (int)(cdiv64(cdiv64(a.RP, nchunks), 64) * 64);
+    return launch_wgrad_kernel<T, H>(a, 2, nchunks, st);
 }
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1198,7 +1292,7 @@ size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
     const int BM = m->dtype == MGN_F32 ? 32 : 64;
     const int64_t ntiles = rows_pad(M) / BM;
-    const int64_t nchunks = cdiv64(rows_pad(M), wgrad_rows_per_chunk(m, M));
+    const int64_t nchunks = wgrad_max_chunks(rows_pad(M));
     size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
     b += align_up((size_t)nchunks * grad_G(m) * sizeof(float));              // wgrad partial slabs
@@ -1253,13 +1347,16 @@ static int mlp_bwd_any(const mgn_mlp* m, int mode, int64_t M, const mgn_mlp_save
 }
 
 static int mlp_wgrad_any(const mgn_mlp* m, int64_t M, const void* act, const void* dz, const float* dsp,
-                         int ntiles, float* part, float* grads, const MlpIn* gin, hipStream_t st) {
+                         int ntiles, float* part, float* grads, const MlpIn* gin, int l0_jobs, int* nchunks,
+                         bool reduce, hipStream_t st) {
     int rc = 0;
+#define MGN_W_CALL(T_) rc = launch_wgrad<T_, HH>(m, M, act, dz, dsp, ntiles, part, grads, gin, l0_jobs, nchunks, reduce, st)
     if (m->dtype == MGN_F32) {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<float, HH>(m, M, act, dz, dsp, ntiles, part, grads, gin, st)))
+        MGN_DISPATCH_H(m->hidden, MGN_W_CALL(float))
     } else {
-        MGN_DISPATCH_H(m->hidden, rc = (launch_wgrad<__bf16, HH>(m, M, act, dz, dsp, ntiles, part, grads, gin, st)))
+        MGN_DISPATCH_H(m->hidden, MGN_W_CALL(__bf16))
     }
+#undef MGN_W_CALL
     return rc;
 }
 
@@ -1282,59 +1379,202 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
         return 0;
     }
     if (int e = mlp_bwd_any(m, mode, M, sv, dout, dout_dtype, dout_ld, o, dz, dsp, st)) return e;
-    return mlp_wgrad_any(m, M, sv->act, dz, dsp, ntiles, part, grads, mode == MODE_DENSE ? nullptr : &in, st);
+    return mlp_wgrad_any(m, M, sv->act, dz, dsp, ntiles, part, grads, mode == MODE_DENSE ? nullptr : &in, 0,
+                         nullptr, true, st);
 }
 
-// =========================================================================== node combine
-// dx[n] = dx_part[n] + Σ_{k in col seg n} dxij[k][0:H] + Σ_{j in row seg n} dxij[row_perm[j]][H:2H]
+// =========================================================================== node side of the edge MLP's layer 0
+// The edge MLP's first Linear acts on [e ‖ x_i ‖ x_j] (layers.py:689-690,717). Its x blocks are
+// applied per NODE instead of per edge: P = [x·W0bᵀ ‖ x·W0cᵀ] (N rows, not E), gathered by the edge
+// kernel's layer-0 epilogue. Backward: dP_i[v] = Σ_{dst(k)=v} dZ0[k], dP_j[v] = Σ_{src(k)=v} dZ0[k],
+// dx += dP_i·W0b + dP_j·W0c, dW0b = dP_iᵀx, dW0c = dP_jᵀx.
+struct ProjArgs {
+    const void* x;      // [N][H] (T)
+    const void* w0;     // forward fragments of the edge layer 0 ([H x 3H])
+    float* proj;        // [N][2H]
+    int64_t N;
+    int32_t ldi, kstride;
+    int32_t wb[2], off[2], ks0[2], nks[2];  // LDS window / leading zero cols / first k-step / k-steps
+};
+
+template <class T, int H, int BM>
+__global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
+    constexpr int NTH = H / 16, MT = BM / 16, VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
+    using G = Gemm<T, NTH, MT>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* In = reinterpret_cast<T*>(smem);
+    const int64_t row0 = (int64_t)blockIdx.x * BM;
+    const int nw = a.wb[1] == a.wb[0] ? 1 : 2;
+    for (int s = 0; s < nw; ++s) {
+        const int lead = a.off[s];
+        for (int it = threadIdx.x; it < BM * lead; it += MGN_THREADS)
+            In[(size_t)(it / lead) * a.ldi + a.wb[s] + it % lead] = from_f<T>(0.f);
+        const SrcSeg g{a.x, nullptr, H, H, dtype_id<T>(), a.wb[s] + lead, 0};
+        load_tile<T, BM>(In, a.ldi, a.wb[s] + lead + H, a.wb[s] + a.nks[s] * KSTEP, &g, 1, row0, a.N);
+    }
+    __syncthreads();
+    const T* w0 = reinterpret_cast<const T*>(a.w0);
+    for (int s = 0; s < 2; ++s) {
+        G g;
+        g.run(w0 + (size_t)a.ks0[s] * 64 * VEC, a.nks[s], In + a.wb[s], a.ldi, false, a.kstride);
+        if (!g.active) continue;
+#pragma unroll
+        for (int j = 0; j < G::C::MTW; ++j) {
+            const int64_t row = row0 + g.m_of(j);
+            if (row >= a.N) continue;
+#pragma unroll
+            for (int i = 0; i < G::C::NTW; ++i)
+                *reinterpret_cast<f4*>(a.proj + row * (2 * H) + s * H + g.n_of(i)) = g.acc[i][j];
+        }
+    }
+}
+
+struct CombArgs {
+    const void* dz0;      // [E][H] (T) dZ of the edge layer 0, target-sorted edges
+    const int32_t* col_ptr;
+    const int32_t* row_ptr;
+    const int32_t* row_perm;
+    const void* dx_part;  // [N][H] (T) node-MLP part of dx
+    const void* wt0;      // transposed fragments of the edge layer 0 ([3H x H])
+    void* dP8;            // R8 [2][RP][H] (T): dP_i, dP_j (weight-gradient operands)
+    void* dx;             // [N][H] (T)
+    int64_t N, RP;
+    int32_t ldb, HP, NS;
+};
+
+template <class T, int H, int BM>
+__global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
+    constexpr int NTH = H / 16, MT = BM / 16, VEC = Mf<T>::VEC;
+    constexpr int CH = 16 / sizeof(T), CPR = H / CH;
+    using G = Gemm<T, NTH, MT>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* B = reinterpret_cast<T*>(smem);  // [BM][ldb]: dP_i at column 0, dP_j at column HP
+    const int64_t row0 = (int64_t)blockIdx.x * BM;
+    const T* dz = reinterpret_cast<const T*>(a.dz0);
+    for (int it = threadIdx.x; it < 2 * BM * CPR; it += MGN_THREADS) {
+        const int s = it / (BM * CPR), rem = it - s * (BM * CPR);
+        const int r = rem / CPR, c = (rem - r * CPR) * CH;
+        const int64_t v = row0 + r;
+        float acc[CH];
+#pragma unroll
+        for (int e = 0; e < CH; ++e) acc[e] = 0.f;
+        if (v < a.N) {
+            const int32_t* ptr = s == 0 ? a.col_ptr : a.row_ptr;
+            const int kb = ptr[v], ke = ptr[v + 1];
+            int k = kb;
+            for (; k + 4 <= ke; k += 4) {
+                float t[4][CH];
+                int64_t src[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) src[u] = s == 0 ? (int64_t)(k + u) : (int64_t)a.row_perm[k + u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
+            }
+            for (; k < ke; ++k) {
+                float t[CH];
+                Chunk<T>::load(dz + (s == 0 ? (int64_t)k : (int64_t)a.row_perm[k]) * H + c, t);
+#pragma unroll
+                for (int e = 0; e < CH; ++e) acc[e] += t[e];
+            }
+        }
+        Chunk<T>::store(B + (size_t)r * a.ldb + s * a.HP + c, acc);
+    }
+    const int padc = a.HP - H;
+    if (padc > 0)
+        for (int it = threadIdx.x; it < 2 * BM * padc; it += MGN_THREADS) {
+            const int s = it / (BM * padc), rem = it - s * (BM * padc);
+            B[(size_t)(rem / padc) * a.ldb + s * a.HP + H + rem % padc] = from_f<T>(0.f);
+        }
+    __syncthreads();
+    for (int s = 0; s < 2; ++s)
+        copy_out_r8<T, BM>(B + s * a.HP, a.ldb, H, reinterpret_cast<T*>(a.dP8) + (int64_t)s * a.RP * H, row0);
+    const T* wt = reinterpret_cast<const T*>(a.wt0);
+    const size_t tile = (size_t)NTH * a.NS * 64 * VEC;  // one H-wide block of transposed tiles
+    G g;
+    g.run(wt + tile, a.NS, B, a.ldb);
+    g.run(wt + 2 * tile, a.NS, B + a.HP, a.ldb, false, 0, true);
+    if (!g.active) return;
+    const T* dxp = reinterpret_cast<const T*>(a.dx_part);
+    T* dx = reinterpret_cast<T*>(a.dx);
+#pragma unroll
+    for (int j = 0; j < G::C::MTW; ++j) {
+        const int64_t row = row0 + g.m_of(j);
+        if (row >= a.N) continue;
+#pragma unroll
+        for (int i = 0; i < G::C::NTW; ++i) {
+            const int n = g.n_of(i);
+            st4(dx + row * H + n, ld4(dxp + row * H + n) + g.acc[i][j]);
+        }
+    }
+}
+
+// layer-0 column window s (1: x_i block, 2: x_j block) of the packed [H x 3H] weight
+template <class T>
+void proj_window(int H, int s, int* ks0, int* nks, int* off) {
+    constexpr int KSTEP = Mf<T>::KSTEP;
+    *ks0 = s * H / KSTEP;
+    *nks = cdiv((s + 1) * H, KSTEP) - *ks0;
+    *off = s * H - *ks0 * KSTEP;
+}
+
 template <class T, int H>
-__global__ __launch_bounds__(MGN_THREADS) void node_combine_kernel(const T* __restrict__ dx_part, const T* __restrict__ dxij,
-                                                                   const int32_t* __restrict__ col_ptr,
-                                                                   const int32_t* __restrict__ row_ptr,
-                                                                   const int32_t* __restrict__ row_perm, int64_t N,
-                                                                   T* __restrict__ dx) {
-    constexpr int CH = 16 / sizeof(T);
-    constexpr int LPN = H / CH;  // lanes per node
-    const int64_t gid = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x;
-    const int64_t n = gid / LPN;
-    const int c = (int)(gid % LPN) * CH;
-    if (n >= N) return;
-    float acc[CH], t[4][CH];
-    Chunk<T>::load(dx_part + n * H + c, acc);
-    const int kb = col_ptr[n], ke = col_ptr[n + 1];
-    int k = kb;
-    for (; k + 4 <= ke; k += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) Chunk<T>::load(dxij + (int64_t)(k + u) * 2 * H + c, t[u]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < CH; ++v) acc[v] += t[u][v];
-    }
-    for (; k < ke; ++k) {
-        Chunk<T>::load(dxij + (int64_t)k * 2 * H + c, t[0]);
-#pragma unroll
-        for (int v = 0; v < CH; ++v) acc[v] += t[0][v];
-    }
-    const int jb = row_ptr[n], je = row_ptr[n + 1];
-    int j = jb;
-    for (; j + 4 <= je; j += 4) {
-        int e4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) e4[u] = row_perm[j + u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) Chunk<T>::load(dxij + (int64_t)e4[u] * 2 * H + H + c, t[u]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < CH; ++v) acc[v] += t[u][v];
-    }
-    for (; j < je; ++j) {
-        Chunk<T>::load(dxij + (int64_t)row_perm[j] * 2 * H + H + c, t[0]);
-#pragma unroll
-        for (int v = 0; v < CH; ++v) acc[v] += t[0][v];
-    }
-    Chunk<T>::store(dx + n * H + c, acc);
+int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, hipStream_t st) {
+    constexpr int BM = bm_of<T>(), KSTEP = Mf<T>::KSTEP;
+    ProjArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = x;
+    a.w0 = edge->wpack;
+    a.proj = proj;
+    a.N = N;
+    a.kstride = cdiv(3 * H, KSTEP);
+    for (int s = 0; s < 2; ++s) proj_window<T>(H, s + 1, &a.ks0[s], &a.nks[s], &a.off[s]);
+    a.wb[0] = 0;
+    const bool shared = a.off[0] == 0 && a.off[1] == 0 && a.nks[0] == a.nks[1];
+    a.wb[1] = shared ? 0 : a.nks[0] * KSTEP;
+    a.ldi = pad_ld<T>(a.wb[1] + a.nks[1] * KSTEP);
+    const size_t lds = (size_t)BM * a.ldi * sizeof(T);
+    auto fn = node_proj_kernel<T, H, BM>;
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    const int grid = (int)(rows_pad(N) / BM);
+    if (grid == 0) return 0;
+    ProfScope ps(PROF_PROJ, st);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+template <class T, int H>
+int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0, const void* dx_part, void* dP8,
+                     void* dx, hipStream_t st) {
+    constexpr int BM = bm_of<T>(), KSTEP = Mf<T>::KSTEP;
+    CombArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dz0 = dz0;
+    a.col_ptr = t->col_ptr;
+    a.row_ptr = t->row_ptr;
+    a.row_perm = t->row_perm;
+    a.dx_part = dx_part;
+    a.wt0 = edge->wtpack;
+    a.dP8 = dP8;
+    a.dx = dx;
+    a.N = t->num_nodes;
+    a.RP = rows_pad(a.N);
+    a.HP = rup(H, KSTEP);
+    a.NS = cdiv(H, KSTEP);
+    a.ldb = pad_ld<T>(2 * a.HP);
+    const size_t lds = (size_t)BM * a.ldb * sizeof(T);
+    auto fn = node_grad_kernel<T, H, BM>;
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    const int grid = (int)(a.RP / BM);
+    if (grid == 0) return 0;
+    ProfScope ps(PROF_COMBINE, st);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(MGN_THREADS), lds, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
 }
 
 // =========================================================================== C ABI
@@ -1384,7 +1624,7 @@ size_t mgn_mlp_backward_workspace_bytes(const mgn_mlp* m, int64_t rows) { return
 
 int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int32_t block_mlp, int64_t* act_elems,
                         int64_t* mask_words) {
-    *act_elems = act_off(*m, rows, m->n_layers, block_mlp && !kSaveBlockInput);
+    *act_elems = act_off(*m, rows, m->n_layers, block_mlp != 0);
     *mask_words = (int64_t)(m->n_layers - 1) * mask_words_per_layer(*m, rows);
     return 0;
 }
@@ -1407,8 +1647,18 @@ int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t
                              (hipStream_t)stream);
 }
 
+static size_t block_fwd_ws(const mgn_topology* t, const mgn_mlp* edge) {
+    return align_up((size_t)t->num_nodes * 2 * edge->hidden * sizeof(float));
+}
+
+size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    (void)node;
+    return block_fwd_ws(t, edge);
+}
+
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
-                      void* x_out, void* e_out, mgn_block_saved* saved, mgn_stream_t stream) {
+                      void* x_out, void* e_out, mgn_block_saved* saved, void* ws, size_t ws_bytes,
+                      mgn_stream_t stream) {
     if (int r = check_mlp(edge)) return r;
     if (int r = check_mlp(node)) return r;
     const int H = edge->hidden;
@@ -1416,17 +1666,32 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     MGN_REQUIRE(node->in_dim == 2 * H && node->out_dim == H && node->hidden == H, "node MLP must be 2h -> h");
     MGN_REQUIRE(saved->edge.z && saved->edge.rden && saved->aggr, "block saved buffers missing");
     MGN_REQUIRE(edge->dtype == node->dtype, "edge/node MLP dtype mismatch");
+    MGN_REQUIRE(ws_bytes >= block_fwd_ws(t, edge) && (ws || t->num_nodes == 0), "block forward workspace too small");
     hipStream_t st = (hipStream_t)stream;
     const int dt = edge->dtype;
+    float* proj = reinterpret_cast<float*>(ws);
+    int rc = 0;
+    if (dt == MGN_F32) {
+        MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, st)))
+    } else {
+        MGN_DISPATCH_H(H, rc = (launch_proj<__bf16, HH>(edge, x, t->num_nodes, proj, st)))
+    }
+    if (rc) return rc;
     MlpIn ein;
     memset(&ein, 0, sizeof(ein));
     ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
-    ein.seg[1] = SrcSeg{x, t->csc_dst, H, H, dt, H, 0};
-    ein.seg[2] = SrcSeg{x, t->csc_src, H, H, dt, 2 * H, 0};
-    ein.nseg = 3;
-    if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr, nullptr,
-                            nullptr, st))
+    ein.nseg = 1;
+    ein.K0 = H;
+    ein.proj = proj;
+    ein.proj_i = t->csc_dst;
+    ein.proj_j = t->csc_src;
+    if (chain_eligible(edge)) {
+        if (int r = chain_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st))
+            return r;
+    } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
+                                   nullptr, nullptr, st)) {
         return r;
+    }
     MlpIn nin;
     memset(&nin, 0, sizeof(nin));
     nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
@@ -1436,28 +1701,34 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
                        saved->aggr, st);
 }
 
-static size_t block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, size_t* off_mlp,
-                             size_t* off_dxpart, size_t* off_daggr, size_t* off_dxij) {
+struct BlockWs {
+    size_t mlp, dxpart, daggr, dz0, dP8, total;
+};
+
+static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
     const size_t es = edge->dtype == MGN_F32 ? 4 : 2;
     const int H = edge->hidden;
     size_t mlp_ws = mlp_bwd_ws(edge, t->num_edges);
     const size_t nws = mlp_bwd_ws(node, t->num_nodes);
     if (nws > mlp_ws) mlp_ws = nws;
+    BlockWs w;
     size_t o = 0;
-    *off_mlp = o;
+    w.mlp = o;
     o += align_up(mlp_ws);
-    *off_dxpart = o;
+    w.dxpart = o;
     o += align_up((size_t)t->num_nodes * H * es);
-    *off_daggr = o;
+    w.daggr = o;
     o += align_up((size_t)t->num_nodes * H * es);
-    *off_dxij = o;
-    o += align_up((size_t)t->num_edges * 2 * H * es);
-    return o;
+    w.dz0 = o;
+    o += align_up((size_t)t->num_edges * H * es);
+    w.dP8 = o;
+    o += align_up((size_t)2 * rows_pad(t->num_nodes) * H * es);
+    w.total = o;
+    return w;
 }
 
 size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
-    size_t a, b, c, d;
-    return block_ws_parts(t, edge, node, &a, &b, &c, &d);
+    return block_ws_parts(t, edge, node).total;
 }
 
 int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
@@ -1465,17 +1736,17 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
                        float* edge_grads, float* node_grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
     if (int r = check_mlp(edge)) return r;
     if (int r = check_mlp(node)) return r;
-    size_t o_mlp, o_dxp, o_dag, o_dij;
-    const size_t need = block_ws_parts(t, edge, node, &o_mlp, &o_dxp, &o_dag, &o_dij);
-    MGN_REQUIRE(ws_bytes >= need, "block backward workspace too small");
+    const BlockWs wl = block_ws_parts(t, edge, node);
+    MGN_REQUIRE(ws_bytes >= wl.total, "block backward workspace too small");
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
     char* w = reinterpret_cast<char*>(ws);
-    void* mlp_ws = w + o_mlp;
-    void* dx_part = w + o_dxp;
-    void* d_aggr = w + o_dag;
-    void* dxij = w + o_dij;
-    const size_t mlp_ws_bytes = o_dxp - o_mlp;
+    void* mlp_ws = w + wl.mlp;
+    void* dx_part = w + wl.dxpart;
+    void* d_aggr = w + wl.daggr;
+    void* dz0 = w + wl.dz0;
+    void* dP8 = w + wl.dP8;
+    const size_t mlp_ws_bytes = wl.dxpart - wl.mlp;
 
     // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
     MlpIn nin;
@@ -1491,40 +1762,55 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on, node_grads,
                                   mlp_ws, mlp_ws_bytes, st))
         return r;
-    // edge MLP: dY = de_out + d_aggr[dst] -> de = de_out + dA0[:, :H], dxij = dA0[:, H:3H]
-    MlpIn ein;
-    memset(&ein, 0, sizeof(ein));
-    ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
-    ein.seg[1] = SrcSeg{x, t->csc_dst, H, H, dt, H, 0};
-    ein.seg[2] = SrcSeg{x, t->csc_src, H, H, dt, 2 * H, 0};
-    ein.nseg = 3;
+    // edge MLP data gradients: dY = de_out + d_aggr[dst] -> de = de_out + dZ0·W0a, dZ0 (row-major)
+    const int64_t E = t->num_edges, N = t->num_nodes;
+    MGN_REQUIRE(mlp_ws_bytes >= mlp_bwd_ws(edge, E), "backward workspace too small");
+    const size_t es = dt == MGN_F32 ? 4 : 2;
+    int ntiles = (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
+    char* p = reinterpret_cast<char*>(mlp_ws);
+    void* dz8 = p;
+    p += align_up((size_t)edge->n_layers * rows_pad(E) * H * es);
+    float* dsp = reinterpret_cast<float*>(p);
+    p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
+    float* part = reinterpret_cast<float*>(p);
     BwdOut oe;
     memset(&oe, 0, sizeof(oe));
     oe.mode = MODE_EDGE;
     oe.gath = d_aggr;
     oe.gath_idx = t->csc_dst;
     oe.o1 = de;
-    oe.o2 = dxij;
-    if (int r = mlp_backward_impl(edge, MODE_EDGE, t->num_edges, ein, &saved->edge, de_out, dt, H, oe, edge_grads,
-                                  mlp_ws, mlp_ws_bytes, st))
-        return r;
-    // dx = dx_part + Σ_col dxi + Σ_row dxj
-    const int64_t N = t->num_nodes;
-    if (N == 0) return 0;
-    const int lpn = H / (int)(16 / (dt == MGN_F32 ? 4 : 2));
-    const unsigned blocks = (unsigned)cdiv64(N * lpn, MGN_THREADS);
-    ProfScope ps(PROF_COMBINE, st);
-    if (dt == MGN_F32) {
-        MGN_DISPATCH_H(H, hipLaunchKernelGGL((node_combine_kernel<float, HH>), dim3(blocks), dim3(MGN_THREADS), 0, st,
-                                             (const float*)dx_part, (const float*)dxij, t->col_ptr, t->row_ptr,
-                                             t->row_perm, N, (float*)dx))
-    } else {
-        MGN_DISPATCH_H(H, hipLaunchKernelGGL((node_combine_kernel<__bf16, HH>), dim3(blocks), dim3(MGN_THREADS), 0,
-                                             st, (const __bf16*)dx_part, (const __bf16*)dxij, t->col_ptr, t->row_ptr,
-                                             t->row_perm, N, (__bf16*)dx))
+    oe.o2 = dz0;
+    if (chain_eligible(edge)) {
+        if (int r = chain_edge_backward(edge, E, &saved->edge, de_out, d_aggr, t->csc_dst, dz8, dsp, &ntiles, de, dz0,
+                                        st))
+            return r;
+    } else if (E > 0) {
+        if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, dz8, dsp, st)) return r;
     }
-    MGN_LAUNCH_CHECK();
-    return 0;
+    // node side: dP = segment sums of dZ0, dx = dx_part + dP_i·W0b + dP_j·W0c
+    int rc = 0;
+    if (dt == MGN_F32) {
+        MGN_DISPATCH_H(H, rc = (launch_node_grad<float, HH>(edge, t, dz0, dx_part, dP8, dx, st)))
+    } else {
+        MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, dz0, dx_part, dP8, dx, st)))
+    }
+    if (rc) return rc;
+    // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
+    MlpIn ein;
+    memset(&ein, 0, sizeof(ein));
+    ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
+    ein.nseg = 1;
+    int nchunks = 0;
+    if (int r = mlp_wgrad_any(edge, E, saved->edge.act, dz8, dsp, ntiles, part, edge_grads, &ein, 1, &nchunks, false,
+                              st))
+        return r;
+    if (dt == MGN_F32) {
+        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<float, HH>(edge, N, dP8, x, part, nchunks, st)))
+    } else {
+        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<__bf16, HH>(edge, N, dP8, x, part, nchunks, st)))
+    }
+    if (rc) return rc;
+    return launch_reduce(edge, part, nchunks, dsp, ntiles, edge_grads, st);
 }
 
 }  // extern "C"

@@ -60,8 +60,10 @@ EXPORTS = {
     "mgn_mlp_saved_elems": (_i32, [ctypes.POINTER(Mlp), _i64, _i32, _vp, _vp]),
     "mgn_mlp_backward": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
                                 ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp]),
+    "mgn_block_forward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
+                                                ctypes.POINTER(Mlp)]),
     "mgn_block_forward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
-                                 _vp, _vp, _vp, _vp, ctypes.POINTER(BlockSaved), _vp]),
+                                 _vp, _vp, _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _sz, _vp]),
     "mgn_block_backward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
                                                  ctypes.POINTER(Mlp)]),
     "mgn_block_backward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
@@ -76,7 +78,7 @@ EXPORTS = {
 }
 
 PROF_KINDS = ["fwd_edge", "fwd_node", "fwd_dense", "bwd_edge", "bwd_node", "bwd_dense", "wgrad",
-              "wgrad_reduce", "combine", "pack", "adamw"]
+              "wgrad_reduce", "combine", "pack", "adamw", "proj"]
 
 
 def profile_enable(on=True):

@@ -262,6 +262,13 @@ def _ws_bytes_block(topo, de, dn):
                                                             ctypes.byref(de), ctypes.byref(dn)))
 
 
+def _fwd_ws_block(topo, de, dn, dev):
+    """Scratch for mgn_block_forward (node projections of the edge MLP's layer 0)."""
+    n = int(nat.lib().mgn_block_forward_workspace_bytes(ctypes.byref(topo.struct), ctypes.byref(de),
+                                                        ctypes.byref(dn)))
+    return torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+
+
 # --------------------------------------------------------------------------- EncodeProcessDecode
 class EPDFunction(torch.autograd.Function):
     """y = EncodeProcessDecode(graph) with the whole processor on libmgn.
@@ -301,6 +308,7 @@ class EPDFunction(torch.autograd.Function):
         xs, es, svs = [x0], [e0], []
         nb = len(bspecs) // 2
         scratch = None
+        fws = _fwd_ws_block(topo, bdescs[0], bdescs[1], dev) if nb else None
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
             if train or scratch is None:
@@ -313,7 +321,8 @@ class EPDFunction(torch.autograd.Function):
             e1 = torch.empty((E, H), dtype=tdt, device=dev)
             nat.check(nat.lib().mgn_block_forward(
                 ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
-                nat.ptr(xs[-1]), nat.ptr(es[-1]), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), st))
+                nat.ptr(xs[-1]), nat.ptr(es[-1]), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), nat.ptr(fws),
+                fws.numel(), st))
             if train:
                 xs.append(x1)
                 es.append(e1)
@@ -415,9 +424,10 @@ class BlockFunction(torch.autograd.Function):
         sv = _alloc_block_saved(pw.descs[0], pw.descs[1], espec, nspec, topo, tdt, dev)
         x1 = torch.empty((N, H), dtype=tdt, device=dev)
         e1 = torch.empty((max(E, 1), H), dtype=tdt, device=dev)
+        fws = _fwd_ws_block(topo, pw.descs[0], pw.descs[1], dev)
         nat.check(nat.lib().mgn_block_forward(
             ctypes.byref(topo.struct), ctypes.byref(pw.descs[0]), ctypes.byref(pw.descs[1]), nat.ptr(x0),
-            nat.ptr(e0), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), st))
+            nat.ptr(e0), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), nat.ptr(fws), fws.numel(), st))
         e_out = _permute(e1, topo.csc_eid, E, H, mdt, x.dtype, True, st) if E else \
             torch.empty((0, H), dtype=x.dtype, device=dev)
         if any(ctx.needs_input_grad):

