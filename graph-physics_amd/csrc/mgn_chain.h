@@ -21,6 +21,7 @@ struct ChainFwdArgs {
     int64_t act_off[4];
     unsigned long long* mask;   // [3][ntiles*64]: lane-owned ReLU bits
     int64_t mask_stride;
+    int32_t ablate;             // diagnostics only (env MGN_ABLATE): 1 loads, 2 R8 saves, 4 MFMA, 8 row stores
 };
 
 struct ChainBwdArgs {
@@ -42,6 +43,7 @@ struct ChainBwdArgs {
     float* dscale_part;         // [grid][128]
     __bf16* de;                 // [M][128] de_out + dZ0·W0a
     __bf16* dz0;                // [M][128] dZ0 row-major
+    int32_t ablate;             // as ChainFwdArgs
 };
 
 bool chain_eligible(const mgn_mlp* m);

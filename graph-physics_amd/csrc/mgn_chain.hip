@@ -102,11 +102,19 @@ __device__ __forceinline__ bf16x8 wfrag(const __bf16* W, int l, int t, int S, in
 }
 
 // acc[t] = Σ_S W(l, t, S) · B[S]
-__device__ __forceinline__ void chain_gemm(f32x16 (&acc)[4], const __bf16* W, int l, const bf16x8 (&B)[8], int lane) {
+__device__ __forceinline__ void chain_gemm(f32x16 (&acc)[4], const __bf16* W, int l, const bf16x8 (&B)[8], int lane,
+                                           bool skip = false) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    if (skip) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = (float)B[2 * t + (r >> 3)][r & 7];
+        return;
+    }
 #pragma unroll
     for (int S = 0; S < 8; ++S)
 #pragma unroll
@@ -115,7 +123,9 @@ __device__ __forceinline__ void chain_gemm(f32x16 (&acc)[4], const __bf16* W, in
 
 // Write the wave's 32x128 tile of values v (D layout) as bf16 into an R8 matrix [RP][128], rows
 // [32*tile, 32*tile + 32): two passes of 16 rows through the wave's scratch.
-__device__ __forceinline__ void store_r8(const f32x16 (&v)[4], __bf16* scr, __bf16* dst, int64_t tile, int lane) {
+__device__ __forceinline__ void store_r8(const f32x16 (&v)[4], __bf16* scr, __bf16* dst, int64_t tile, int lane,
+                                         int ablate = 0) {
+    if (ablate & 2) return;
     const int m = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -150,7 +160,8 @@ __device__ __forceinline__ void store_r8(const f32x16 (&v)[4], __bf16* scr, __bf
 // Write the wave's tile of values v (D layout) as bf16 rows into a row-major [M][128] matrix
 // (rows >= M skipped), as coalesced 16-byte row chunks through the scratch.
 __device__ __forceinline__ void store_rows(const f32x16 (&v)[4], __bf16* scr, __bf16* dst, int64_t tile, int64_t M,
-                                           int lane) {
+                                           int lane, int ablate = 0) {
+    if (ablate & 8) return;
     const int m = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -190,6 +201,7 @@ struct FwdProj {
 __device__ __forceinline__ int64_t clamp_row(const int64_t row, int64_t M) { return row < M ? row : M - 1; }
 
 __device__ __forceinline__ void fwd_load(FwdIn& in, const ChainFwdArgs& a, int64_t tile, int lane) {
+    if (a.ablate & 1) tile = 0;  // diagnostics: every tile reads tile 0 (cache-resident)
     const int m = lane & 31, h = lane >> 5;
     const int64_t row = clamp_row(tile * TR + m, a.M);
     const __bf16* e = a.e + row * H + 4 * h;
@@ -216,32 +228,45 @@ __device__ __forceinline__ void fwd_proj(FwdProj& in, const ChainFwdArgs& a, int
 }
 
 __device__ __forceinline__ void fwd_idx(const ChainFwdArgs& a, int64_t tile, int lane, int& di, int& dj) {
+    if (a.ablate & 1) tile = 0;
     const int64_t row = clamp_row(tile * TR + (lane & 31), a.M);
     di = a.proj_i[row];
     dj = a.proj_j[row];
 }
 
-// hidden-layer epilogue: v = relu(acc + bias (+ proj)); mask bits; next B operand; R8 save
+// w = 2w + (v > 0): v_cmp to VCC, then add-with-carry — two instructions, no bit constants. After
+// 32 pushes, element k of the word sits at bit 31 - k.
+__device__ __forceinline__ unsigned push_bit(unsigned w, float v) {
+    unsigned r;
+    asm("v_cmp_lt_f32 vcc, 0, %2\n\tv_addc_co_u32 %0, vcc, %1, %1, vcc" : "=v"(r) : "v"(w), "v"(v) : "vcc");
+    return r;
+}
+
+// all-ones if element k (0..31, pushed k-th) of w is set, else 0
+__device__ __forceinline__ int bit_sel(unsigned w, int k) { return (int)(w << k) >> 31; }
+
+// hidden-layer epilogue: v = relu(acc + bias), or relu(acc + P_i + P_j) for layer 0 (the node
+// projection P_i carries b0); mask bits; next B operand.
 __device__ __forceinline__ void fwd_hidden(f32x16 (&acc)[4], const float* bias, const FwdProj* in, bf16x8 (&B)[8],
-                                           uint64_t& bits, int lane) {
+                                           uint2& bits, int lane) {
     const int h = lane >> 5;
-    bits = 0;
+    unsigned w[2] = {0u, 0u};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const f4 b = *reinterpret_cast<const f4*>(bias + 32 * t + 8 * g + 4 * h);
+            const f4 b = in ? in->pi[4 * t + g] + in->pj[4 * t + g]
+                            : *reinterpret_cast<const f4*>(bias + 32 * t + 8 * g + 4 * h);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int r = 4 * g + i;
-                float z = acc[t][r] + b[i];
-                if (in) z += in->pi[4 * t + g][i] + in->pj[4 * t + g][i];
-                const float v = fmaxf(z, 0.f);
+                const int r = 4 * g + i, k = 16 * t + r;
+                const float v = fmaxf(acc[t][r] + b[i], 0.f);
                 acc[t][r] = v;
-                bits |= (uint64_t)(v > 0.f) << (16 * t + r);
+                w[k >> 5] = push_bit(w[k >> 5], v);
                 B[2 * t + (r >> 3)][r & 7] = (__bf16)v;
             }
         }
+    bits = make_uint2(w[0], w[1]);
 }
 
 __global__ __launch_bounds__(NW * 64) void chain_fwd_kernel(ChainFwdArgs a) {
@@ -276,23 +301,24 @@ __global__ __launch_bounds__(NW * 64) void chain_fwd_kernel(ChainFwdArgs a) {
         fwd_idx(a, min(tile + stride, last), lane, ndi, ndj);
         fwd_load(nxt, a, min(tile + stride, last), lane);
         const int64_t row = tile * TR + m;
-        f32x16 acc[4];
+        f32x16 accs[1][4];
         bf16x8 B[8];
-        uint64_t bits;
+        uint2 bits;
         // layer 0: e·W0aᵀ + P_i[dst] + P_j[src] + b0
-        chain_gemm(acc, W, 0, in.eb, lane);
-        fwd_hidden(acc, vec, &pr, B, bits, lane);
-        a.mask[tile * 64 + lane] = bits;
-        store_r8(acc, scr, a.act8 + a.act_off[1], tile, lane);
+        chain_gemm(accs[0], W, 0, in.eb, lane, a.ablate & 4);
+        fwd_hidden(accs[0], vec, &pr, B, bits, lane);
+        reinterpret_cast<uint2*>(a.mask)[tile * 64 + lane] = bits;
+        store_r8(accs[0], scr, a.act8 + a.act_off[1], tile, lane, a.ablate);
 #pragma unroll
         for (int l = 1; l < 3; ++l) {
-            chain_gemm(acc, W, l, B, lane);
-            fwd_hidden(acc, vec + l * H, nullptr, B, bits, lane);
-            a.mask[l * a.mask_stride + tile * 64 + lane] = bits;
-            store_r8(acc, scr, a.act8 + a.act_off[l + 1], tile, lane);
+            chain_gemm(accs[0], W, l, B, lane, a.ablate & 4);
+            fwd_hidden(accs[0], vec + l * H, nullptr, B, bits, lane);
+            reinterpret_cast<uint2*>(a.mask)[l * a.mask_stride + tile * 64 + lane] = bits;
+            store_r8(accs[0], scr, a.act8 + a.act_off[l + 1], tile, lane, a.ablate);
         }
         // layer 3 + RMSNorm + residual
-        chain_gemm(acc, W, 3, B, lane);
+        f32x16 (&acc)[4] = accs[0];
+        chain_gemm(acc, W, 3, B, lane, a.ablate & 4);
         float ss = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -308,8 +334,9 @@ __global__ __launch_bounds__(NW * 64) void chain_fwd_kernel(ChainFwdArgs a) {
             }
         ss += __shfl_xor(ss, 32);
         const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        const float rq = __builtin_amdgcn_rcpf(q);  // bf16 outputs: z·(1/q) is within 2 fp32 ulp of z/q
         if (h == 0 && row < a.M) a.rden_save[row] = q;
-        store_rows(acc, scr, a.z_save, tile, a.M, lane);
+        store_rows(acc, scr, a.z_save, tile, a.M, lane, a.ablate);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -318,10 +345,10 @@ __global__ __launch_bounds__(NW * 64) void chain_fwd_kernel(ChainFwdArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int r = 4 * g + i;
-                    acc[t][r] = (float)in.eb[2 * t + (r >> 3)][r & 7] + s[i] * (acc[t][r] / q);
+                    acc[t][r] = fmaf(s[i], acc[t][r] * rq, (float)in.eb[2 * t + (r >> 3)][r & 7]);
                 }
             }
-        store_rows(acc, scr, a.out, tile, a.M, lane);
+        store_rows(acc, scr, a.out, tile, a.M, lane, a.ablate);
 #pragma unroll
         for (int S = 0; S < 8; ++S) pin(nxt.eb[S]);
         pin(ndi);
@@ -337,6 +364,7 @@ struct BwdIn {   // raw bf16: features dcol(t, 4g, h)..+3, index t*4 + g
     u32x2 g[16];    // d_aggr[dst(row)]
     u32x2 z[16];    // z[row]
     float q;
+    uint2 mask[3];     // ReLU bits of hidden layers 0..2 (forward layout)
 };
 
 __device__ __forceinline__ f4 bf4(u32x2 v) {
@@ -345,6 +373,7 @@ __device__ __forceinline__ f4 bf4(u32x2 v) {
 }
 
 __device__ __forceinline__ void bwd_load(BwdIn& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
+    if (a.ablate & 1) tile = 0;  // diagnostics: every tile reads tile 0 (cache-resident)
     const int m = lane & 31, h = lane >> 5;
     const int64_t row = clamp_row(tile * TR + m, a.M);
     const __bf16* d = a.dout + row * H + 4 * h;
@@ -358,9 +387,12 @@ __device__ __forceinline__ void bwd_load(BwdIn& in, const ChainBwdArgs& a, int64
         in.z[q] = *reinterpret_cast<const u32x2*>(z + off);
     }
     in.q = a.rden_save[row];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) in.mask[l] = reinterpret_cast<const uint2*>(a.mask)[l * a.mask_stride + tile * 64 + lane];
 }
 
 __device__ __forceinline__ int bwd_idx(const ChainBwdArgs& a, int64_t tile, int lane) {
+    if (a.ablate & 1) tile = 0;
     return a.gath_idx[clamp_row(tile * TR + (lane & 31), a.M)];
 }
 
@@ -393,6 +425,8 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
             pin(nxt.z[q]);
         }
         pin(nxt.q);
+#pragma unroll
+        for (int l = 0; l < 3; ++l) pin(nxt.mask[l]);
         pin(ngi);
     }
     for (; tile < a.ntiles; tile += stride) {
@@ -400,7 +434,8 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
         const bool ok = row < a.M;
         // RMSNorm backward (layers.py:59-74): dz = s·dy/q − z·(Σ s·dy·z)/(q²·rms)·(1/H), from the
         // prefetched tile; its registers are then free for the next tile's prefetch.
-        f32x16 acc[4];  // dy, then dz
+        f32x16 accs[1][4];
+        f32x16 (&acc)[4] = accs[0];  // dy, then dz
         float dot = 0.f;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -415,6 +450,7 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
         }
         dot += __shfl_xor(dot, 32);
         const float qd = nxt.q;
+        const float rq = __builtin_amdgcn_rcpf(qd);  // bf16 dZ: ·(1/q) within 2 fp32 ulp of /q
         const float rms = qd - RMS_EPS;
         const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
         bf16x8 B[8];
@@ -426,8 +462,8 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
             for (int i = 0; i < 4; ++i) {
                 const int t = q >> 2, r = 4 * (q & 3) + i;
                 const float dy = acc[t][r];
-                const float dz = ok ? sc[i] * dy / qd - z[i] * coef : 0.f;
-                dsc[q][i] += ok ? dy * (z[i] / qd) : 0.f;
+                const float dz = ok ? fmaf(-z[i], coef, sc[i] * dy * rq) : 0.f;
+                dsc[q][i] = fmaf(ok ? dy * z[i] : 0.f, rq, dsc[q][i]);
                 acc[t][r] = dz;
                 B[2 * t + (r >> 3)][r & 7] = (__bf16)dz;
             }
@@ -435,29 +471,34 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
         u32x2 dcur[16];  // de_out of this tile, for the layer-0 residual
 #pragma unroll
         for (int q = 0; q < 16; ++q) dcur[q] = nxt.d[q];
+        uint2 mcur[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : make_uint2(0u, 0u);
         __builtin_amdgcn_sched_barrier(0);
         bwd_load(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bwd_idx(a, min(tile + 2 * stride, last), lane);
-        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
+        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane, a.ablate);
         // layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_l > 0]
 #pragma unroll
         for (int l = 3; l >= 1; --l) {
-            chain_gemm(acc, W, l, B, lane);
-            const uint64_t w = a.mask[(l - 1) * a.mask_stride + tile * 64 + lane];
-            const uint64_t bits = ok ? w : 0ull;
+            f32x16 (&c)[4] = accs[0];
+            chain_gemm(c, W, l, B, lane, a.ablate & 4);
+            const unsigned bw[2] = {mcur[l - 1].x, mcur[l - 1].y};
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float v = ((bits >> (16 * t + r)) & 1ull) ? acc[t][r] : 0.f;
-                    acc[t][r] = v;
+                    const int k = 16 * t + r;  // bit -> all-ones / zero lane mask (v_bfe_i32), then AND
+                    const int sel = bit_sel(bw[k >> 5], k & 31);
+                    const float v = __int_as_float(__float_as_int(c[t][r]) & sel);
+                    c[t][r] = v;
                     B[2 * t + (r >> 3)][r & 7] = (__bf16)v;
                 }
-            store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
-            if (l == 1) store_rows(acc, scr, a.dz0, tile, a.M, lane);
+            store_r8(c, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane, a.ablate);
+            if (l == 1) store_rows(c, scr, a.dz0, tile, a.M, lane, a.ablate);
         }
         // layer 0, e block: de = de_out + dZ0 · W0a
-        chain_gemm(acc, W, 0, B, lane);
+        chain_gemm(acc, W, 0, B, lane, a.ablate & 4);
         // rows past M are not stored
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -467,7 +508,7 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[t][4 * g + i] = o[i] + acc[t][4 * g + i];
             }
-        store_rows(acc, scr, a.de, tile, a.M, lane);
+        store_rows(acc, scr, a.de, tile, a.M, lane, a.ablate);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             pin(nxt.d[q]);
@@ -475,6 +516,8 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
             pin(nxt.z[q]);
         }
         pin(nxt.q);
+#pragma unroll
+        for (int l = 0; l < 3; ++l) pin(nxt.mask[l]);
         pin(ngi2);
         ngi = ngi2;
     }
@@ -512,6 +555,12 @@ int set_lds_once(const void* fn, size_t bytes) {
     MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     done[slot] = true;
     return 0;
+}
+
+// diagnostics only: MGN_ABLATE (results are wrong when nonzero)
+int ablate_env() {
+    const char* e = getenv("MGN_ABLATE");
+    return e ? atoi(e) : 0;
 }
 
 int chain_grid(int64_t ntiles) {
@@ -567,6 +616,7 @@ int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const
     for (int l = 0; l < 4; ++l) a.act_off[l] = act_off(*m, M, l, 1);
     a.mask = reinterpret_cast<unsigned long long*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
+    a.ablate = ablate_env();
     if (a.ntiles == 0) return 0;
     if (int e2 = set_lds_once((const void*)chain_fwd_kernel, LDS_TOTAL)) return e2;
     ProfScope ps(PROF_FWD_EDGE, st);
@@ -598,6 +648,7 @@ int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, co
     a.dscale_part = dscale_part;
     a.de = reinterpret_cast<__bf16*>(de);
     a.dz0 = reinterpret_cast<__bf16*>(dz0);
+    a.ablate = ablate_env();
     *nparts = 0;
     if (a.ntiles == 0) return 0;
     if (int e2 = set_lds_once((const void*)chain_bwd_kernel, LDS_TOTAL)) return e2;

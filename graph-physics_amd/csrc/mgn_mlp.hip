@@ -1392,6 +1392,7 @@ struct ProjArgs {
     const void* x;      // [N][H] (T)
     const void* w0;     // forward fragments of the edge layer 0 ([H x 3H])
     float* proj;        // [N][2H]
+    const float* bias0; // optional: b0 folded into the x_i block (the chained edge kernel's layer 0)
     int64_t N;
     int32_t ldi, kstride;
     int32_t wb[2], off[2], ks0[2], nks[2];  // LDS window / leading zero cols / first k-step / k-steps
@@ -1423,8 +1424,11 @@ __global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
             const int64_t row = row0 + g.m_of(j);
             if (row >= a.N) continue;
 #pragma unroll
-            for (int i = 0; i < G::C::NTW; ++i)
-                *reinterpret_cast<f4*>(a.proj + row * (2 * H) + s * H + g.n_of(i)) = g.acc[i][j];
+            for (int i = 0; i < G::C::NTW; ++i) {
+                f4 v = g.acc[i][j];
+                if (s == 0 && a.bias0) v += ld4u(a.bias0 + g.n_of(i));
+                *reinterpret_cast<f4*>(a.proj + row * (2 * H) + s * H + g.n_of(i)) = v;
+            }
         }
     }
 }
@@ -1522,13 +1526,14 @@ void proj_window(int H, int s, int* ks0, int* nks, int* off) {
 }
 
 template <class T, int H>
-int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, hipStream_t st) {
+int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, const float* bias0, hipStream_t st) {
     constexpr int BM = bm_of<T>(), KSTEP = Mf<T>::KSTEP;
     ProjArgs a;
     memset(&a, 0, sizeof(a));
     a.x = x;
     a.w0 = edge->wpack;
     a.proj = proj;
+    a.bias0 = bias0;
     a.N = N;
     a.kstride = cdiv(3 * H, KSTEP);
     for (int s = 0; s < 2; ++s) proj_window<T>(H, s + 1, &a.ks0[s], &a.nks[s], &a.off[s]);
@@ -1670,11 +1675,13 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     hipStream_t st = (hipStream_t)stream;
     const int dt = edge->dtype;
     float* proj = reinterpret_cast<float*>(ws);
+    const bool chain = chain_eligible(edge);
+    const float* b0 = chain ? edge->bias[0] : nullptr;  // the chained kernel takes b0 from P_i
     int rc = 0;
     if (dt == MGN_F32) {
-        MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, st)))
+        MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, b0, st)))
     } else {
-        MGN_DISPATCH_H(H, rc = (launch_proj<__bf16, HH>(edge, x, t->num_nodes, proj, st)))
+        MGN_DISPATCH_H(H, rc = (launch_proj<__bf16, HH>(edge, x, t->num_nodes, proj, b0, st)))
     }
     if (rc) return rc;
     MlpIn ein;
@@ -1685,7 +1692,7 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     ein.proj = proj;
     ein.proj_i = t->csc_dst;
     ein.proj_j = t->csc_src;
-    if (chain_eligible(edge)) {
+    if (chain) {
         if (int r = chain_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st))
             return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
