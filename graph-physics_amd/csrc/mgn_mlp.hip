@@ -758,8 +758,25 @@ struct WgArgs {
     int64_t G;
 };
 
+// Two groups of 4 waves per workgroup split the chunk's rows (alternate k-steps / stages) and
+// combine their tiles through LDS in a fixed order: twice the resident waves of a 4-wave
+// workgroup without more partial slabs.
+constexpr int WG_GROUPS = 2;
+
 template <class T, int H>
-__global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
+constexpr int wg_tile_floats() {
+    return TileCfg<H / 16, H / 16>::NTW * TileCfg<H / 16, H / 16>::MTW * 4 + TileCfg<H / 16, H / 16>::NTW;
+}
+
+template <class T, int H>
+size_t wgrad_lds_bytes(bool staged) {
+    const size_t stage = staged ? (size_t)WG_GROUPS * 2 * H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
+    const size_t red = (size_t)MGN_THREADS * wg_tile_floats<T, H>() * sizeof(float);
+    return stage > red ? stage : red;
+}
+
+template <class T, int H>
+__global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
     constexpr int NT = H / 16;
     constexpr int SR = 64;                      // rows per LDS stage (re-gathered layer-0 input)
@@ -767,11 +784,12 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int LDT = SR + CH;                // LDS row = one input column over SR rows (+pad)
     using C = TileCfg<NT, NT>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* AT = reinterpret_cast<T*>(smem);         // [H][LDT]
+    const int grp = threadIdx.x / MGN_THREADS, tid = threadIdx.x % MGN_THREADS;
+    T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * H * LDT;  // this group's [2][H][LDT]
     const WgJob job = a.job[blockIdx.y];
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
     const int64_t r_end = r_begin + a.rows_per_chunk < a.RP ? r_begin + a.rows_per_chunk : a.RP;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = tid & 63, wave = tid >> 6;
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
     const bool active = mt0 < NT;
@@ -805,7 +823,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
     };
     if (!staged) {
 #pragma unroll 2
-        for (int64_t m0 = r_begin; m0 < r_end; m0 += KSTEP) {
+        for (int64_t m0 = r_begin + grp * KSTEP; m0 < r_end; m0 += WG_GROUPS * KSTEP) {
             if (!active) break;
             const int64_t mr = m0 + VEC * (lane >> 4);
             typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
@@ -829,6 +847,8 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
         // consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the transposed
         // LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots: conflict-free.
         // Double buffered: the next stage's loads are in flight while this stage's MFMAs run.
+        // The groups take alternate SR-row stages; both run the same number of iterations (a group
+        // past the end stages zeros) so every workgroup barrier is reached by all threads.
         constexpr int ITEMS = SR * (H / CH);
         constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;  // 16-byte chunks per thread
 
@@ -836,7 +856,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
         auto issue = [&](int64_t m0) {
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const int it = threadIdx.x + q * MGN_THREADS;
+                const int it = tid + q * MGN_THREADS;
                 const int r = it % SR, cc = (it / SR) * CH;
                 const int64_t row = m0 + r;
                 nxt[q] = u32x4{0u, 0u, 0u, 0u};
@@ -846,12 +866,13 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
                 }
             }
         };
-        issue(r_begin);
-        for (int64_t m0 = r_begin; m0 < r_end; m0 += SR) {
-            T* buf = AT + (size_t)((m0 - r_begin) / SR & 1) * H * LDT;
+        issue(r_begin + grp * SR);
+        for (int64_t base = r_begin; base < r_end; base += WG_GROUPS * SR) {
+            const int64_t m0 = base + grp * SR;
+            T* buf = AT + (size_t)((base - r_begin) / (WG_GROUPS * SR) & 1) * H * LDT;
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const int it = threadIdx.x + q * MGN_THREADS;
+                const int it = tid + q * MGN_THREADS;
                 if (it >= ITEMS) continue;
                 const int r = it % SR, cc = (it / SR) * CH;
                 const T* v = reinterpret_cast<const T*>(&nxt[q]);
@@ -859,8 +880,8 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
                 for (int e = 0; e < CH; ++e) buf[(size_t)(cc + e) * LDT + r] = v[e];
             }
             __syncthreads();
-            issue(m0 + SR);
-            if (active) {
+            issue(m0 + WG_GROUPS * SR);
+            if (active && m0 < r_end) {
 #pragma unroll
                 for (int ks = 0; ks < SR / KSTEP; ++ks) {
                     const int64_t mr = m0 + ks * KSTEP + VEC * (lane >> 4);
@@ -879,7 +900,31 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_wgrad_kernel(WgArgs a) {
             }
         }
     }
-    if (!active) return;
+    // group 1 hands its tile to group 0 through LDS (layout [value][thread]: conflict-free)
+    constexpr int TF = wg_tile_floats<T, H>();
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // staging buffers are dead
+    if (grp == 1) {
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i) {
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[((i * C::MTW + j) * 4 + r) * MGN_THREADS + tid] = acc[i][j][r];
+            red[(C::NTW * C::MTW * 4 + i) * MGN_THREADS + tid] = bsum[i];
+        }
+    }
+    __syncthreads();
+    if (grp == 1 || !active) return;
+#pragma unroll
+    for (int i = 0; i < C::NTW; ++i) {
+#pragma unroll
+        for (int j = 0; j < C::MTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((i * C::MTW + j) * 4 + r) * MGN_THREADS + tid];
+        bsum[i] += red[(C::NTW * C::MTW * 4 + i) * MGN_THREADS + tid];
+    }
+    static_assert(TF == C::NTW * C::MTW * 4 + C::NTW, "tile layout");
     float* part = a.part + (int64_t)blockIdx.x * a.G;
 #pragma unroll
     for (int i = 0; i < C::NTW; ++i)
@@ -1191,10 +1236,11 @@ template <class T, int H>
 int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
     a.njobs = nj;
     auto fn = mlp_wgrad_kernel<T, H>;
-    const size_t lds = a.gathered ? 2 * (size_t)H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
+    const size_t lds = wgrad_lds_bytes<T, H>(a.gathered != 0);
+    if (int e = set_lds((const void*)fn, wgrad_lds_bytes<T, H>(true))) return e;
     if (nchunks > 0 && nj > 0) {
         ProfScope ps(PROF_WGRAD, st);
-        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS), lds, st, a);
+        hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS * WG_GROUPS), lds, st, a);
         MGN_LAUNCH_CHECK();
     }
     return 0;
