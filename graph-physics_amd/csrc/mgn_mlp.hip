@@ -1031,6 +1031,10 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 // --------------------------------------------------------------------------- host side
 template <class T>
 constexpr int bm_of() { return sizeof(T) == 4 ? 32 : 64; }
+// rows per workgroup tile: bf16 node MLPs use 32 (N is ~6x smaller than E: twice the workgroups)
+template <class T, int MODE>
+constexpr int bm_for() { return MODE == MODE_NODE ? 32 : bm_of<T>(); }
+int bm_host(int dtype, int mode) { return dtype == MGN_F32 || mode == MODE_NODE ? 32 : 64; }
 
 // Raise a kernel's dynamic-LDS limit once (not per launch: launches may be inside a graph capture).
 int set_lds(const void* fn, size_t bytes) {
@@ -1080,7 +1084,7 @@ template <class T, int H, int MODE>
 int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_dtype, int64_t out_ld,
                const void* resid, mgn_mlp_saved* sv, const mgn_topology* topo, const mgn_mlp* agg_mlp,
                const mgn_mlp_saved* agg_sv, void* agg_save, hipStream_t st) {
-    constexpr int BM = bm_of<T>();
+    constexpr int BM = bm_for<T, MODE>();
     FwdArgs a;
     memset(&a, 0, sizeof(a));
     for (int s = 0; s < in.nseg; ++s) a.seg[s] = in.seg[s];
@@ -1150,7 +1154,7 @@ struct BwdOut {
 template <class T, int H, int MODE>
 int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, int dout_dtype,
                int64_t dout_ld, const BwdOut& o, void* dz_save, float* dscale_part, hipStream_t st) {
-    constexpr int BM = bm_of<T>();
+    constexpr int BM = bm_for<T, MODE>();
     BwdArgs a;
     memset(&a, 0, sizeof(a));
     a.M = M;
@@ -1336,8 +1340,7 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
-    const int BM = m->dtype == MGN_F32 ? 32 : 64;
-    const int64_t ntiles = rows_pad(M) / BM;
+    const int64_t ntiles = rows_pad(M) / 32;  // dscale partial rows: the smallest tile over modes
     const int64_t nchunks = wgrad_max_chunks(rows_pad(M));
     size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
@@ -1412,8 +1415,7 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
                              void* ws, size_t ws_bytes, hipStream_t st) {
     MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, M), "backward workspace too small");
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
-    const int BM = m->dtype == MGN_F32 ? 32 : 64;
-    const int ntiles = (int)(rows_pad(M) / BM);
+    const int ntiles = (int)(rows_pad(M) / bm_host(m->dtype, mode));
     char* p = reinterpret_cast<char*>(ws);
     void* dz = p;
     p += align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);
