@@ -52,7 +52,25 @@ def parse():
 
 
 def flops_per_block(n, e, h):
-    return 12 * h * h * e, 10 * h * h * n  # edge MLP, node MLP (2·Σ in·out per row)
+    # MFMA FLOPs per launch (2·Σ in·out per row). The edge MLP's layer 0 runs on the e block only
+    # (the x blocks are applied per node: node_proj / node_grad kernels), so 4 128x128 Linears.
+    return 8 * h * h * e, 10 * h * h * n  # edge MLP, node MLP
+
+
+def bytes_per_block(n, e, h, es):
+    """Compulsory HBM bytes per launch of the block kernels (SURVEY §8d unit = one edge / node):
+    every input read once, every output written once, gathered rows counted once per use at their
+    stored size; es = activation element size (2 bf16, 4 fp32)."""
+    mask = 3 * h // 8  # ReLU bits of the 3 hidden layers
+    edge_fwd = e * (es * h + es * h * 2 + 3 * es * h + mask + 4 + 2 * 4 * h)
+    # e in | out, z | R8 inputs of layers 1..3 | masks | rden | fp32 node projections P_i, P_j gathered
+    edge_bwd = e * (3 * es * h + 4 + mask + 4 * es * h + 2 * es * h)
+    # de_out, d_aggr[dst], z in | rden | masks | dZ of 4 layers (R8) | de, dZ0 row-major out
+    node_fwd = e * (es * h + 4) + n * (es * h + 3 * es * h + 4 + mask + 3 * es * h)
+    # edge z + rden (segment sum) | x in; x_out, aggr, z out; rden; masks; R8 inputs of layers 1..3
+    node_bwd = n * (es * h + es * h + 4 + mask + 4 * es * h + 2 * es * h)
+    # dx_out, z in | rden | masks | dZ of 4 layers (R8) | dx_part, d_aggr out
+    return {"fwd_edge": edge_fwd, "bwd_edge": edge_bwd, "fwd_node": node_fwd, "bwd_node": node_bwd}
 
 
 def main():
@@ -140,6 +158,7 @@ def main():
 
     h = a.hidden
     fe, fn = flops_per_block(N, E, h)
+    alg_bytes = bytes_per_block(N, E, h, 2 if a.dtype == "bf16" else 4)
     kinds = {}
     for k, (ms, cnt) in prof.items():
         if cnt:
@@ -150,10 +169,14 @@ def main():
     if kinds:
         dom = max((k for k in kinds if k in alg_flops), key=lambda k: kinds[k]["total_ms"])
         avg_s = kinds[dom]["total_ms"] / 1000 / kinds[dom]["launches"]
-        ach = alg_flops[dom] / avg_s / 1e12
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[a.dtype],
-                "unit": "TFLOP/s", "frac": round(ach / PEAK[a.dtype], 4), "traffic": None,
-                "flops_per_launch": alg_flops[dom], "avg_launch_us": round(avg_s * 1e6, 2)}
+        tf = alg_flops[dom] / avg_s / 1e12
+        gbs = alg_bytes[dom] / avg_s / 1e9
+        mfma = {"achieved": round(tf, 2), "peak": PEAK[a.dtype], "unit": "TFLOP/s", "frac": round(tf / PEAK[a.dtype], 4)}
+        hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbs / HBM_PEAK, 4)}
+        bound = "hbm" if hbm["frac"] >= mfma["frac"] else "mfma"
+        roof = {"kernel": dom, "bound": bound, **(hbm if bound == "hbm" else mfma), "traffic": None,
+                "bytes_per_launch": alg_bytes[dom], "flops_per_launch": alg_flops[dom],
+                "avg_launch_us": round(avg_s * 1e6, 2), "hbm": hbm, "mfma": mfma}
         step_flops = 3 * (a.mp * (fe + fn) + 2 * (3 * h + 3 * h * h) * E + 2 * (11 * h + 3 * h * h) * N
                           + 2 * (3 * h * h + h * 2) * N)
         roof["step_tflops_per_s"] = round(step_flops * a.steps / dt / 1e12, 2)

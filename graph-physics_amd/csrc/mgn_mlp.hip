@@ -1575,7 +1575,7 @@ void proj_window(int H, int s, int* ks0, int* nks, int* off) {
 
 template <class T, int H>
 int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, const float* bias0, hipStream_t st) {
-    constexpr int BM = bm_of<T>(), KSTEP = Mf<T>::KSTEP;
+    constexpr int BM = bm_for<T, MODE_NODE>(), KSTEP = Mf<T>::KSTEP;
     ProjArgs a;
     memset(&a, 0, sizeof(a));
     a.x = x;
@@ -1603,7 +1603,7 @@ int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, cons
 template <class T, int H>
 int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0, const void* dx_part, void* dP8,
                      void* dx, hipStream_t st) {
-    constexpr int BM = bm_of<T>(), KSTEP = Mf<T>::KSTEP;
+    constexpr int BM = bm_for<T, MODE_NODE>(), KSTEP = Mf<T>::KSTEP;
     CombArgs a;
     memset(&a, 0, sizeof(a));
     a.dz0 = dz0;

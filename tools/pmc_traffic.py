@@ -31,8 +31,10 @@ def kernel_class(name):
     m = re.search(r"mlp_(fwd|bwd)_kernel.*?Li(\d+)ELi(\d+)ELi(\d)E", name)
     if m:
         return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[m.group(4)]
-    for key, cls in (("mlp_wgrad_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
-                     ("node_combine_kernel", "combine"), ("adamw", "adamw"), ("pack_kernel", "pack")):
+    for key, cls in (("chain_fwd_kernel", "fwd_edge"), ("chain_bwd_kernel", "bwd_edge"),
+                     ("mlp_wgrad_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
+                     ("node_grad_kernel", "combine"), ("node_proj_kernel", "proj"),
+                     ("adamw", "adamw"), ("pack_kernel", "pack")):
         if key in name:
             return cls
     return None
