@@ -133,6 +133,47 @@ __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, c
 
 }  // namespace
 
+
+// Column statistics of a row-major fp32 matrix: per block, fixed row range, per-thread strided rows,
+// LDS tree in fixed order -> part[block][2*cols] (sum, sum of squares); a one-block pass then sums
+// the partials in block order. Deterministic for given (rows, cols).
+constexpr int STAT_MAXC = 32;
+constexpr int STAT_BLOCKS = 256;
+
+__global__ __launch_bounds__(256) void colstats_partial(const float* __restrict__ x, int64_t rows, int cols, int64_t ld,
+                                                        int64_t rows_per_block, float* __restrict__ part) {
+    __shared__ float red[256];
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    for (int c = 0; c < cols; ++c) {
+        float s = 0.f, s2 = 0.f;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+            const float v = x[r * ld + c];
+            s += v;
+            s2 = fmaf(v, v, s2);
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            red[threadIdx.x] = pass ? s2 : s;
+            __syncthreads();
+            for (int w = 128; w > 0; w >>= 1) {
+                if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) part[(int64_t)blockIdx.x * 2 * cols + pass * cols + c] = red[0];
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void colstats_final(const float* __restrict__ part, int nblocks, int cols,
+                                                     float* __restrict__ out) {
+    const int i = threadIdx.x;
+    if (i >= 2 * cols) return;
+    float t = 0.f;
+    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * 2 * cols + i];
+    out[i] = t;
+}
+
 extern "C" {
 
 int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
@@ -241,6 +282,29 @@ int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
     hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
                        exp_avg_sq, n, decay, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
                        (float)bc2_sqrt, (float)eps, (float)(-step_size));
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+
+size_t mgn_column_stats_workspace_bytes(int64_t rows, int32_t cols) {
+    (void)rows;
+    return (size_t)STAT_BLOCKS * 2 * (cols > 0 ? cols : 1) * sizeof(float);
+}
+
+int mgn_column_stats(const float* x, int64_t rows, int32_t cols, int64_t ld, float* sums, void* ws, size_t ws_bytes,
+                     mgn_stream_t stream) {
+    MGN_REQUIRE(cols >= 1 && cols <= STAT_MAXC, "column_stats: cols must be in [1, 32]");
+    MGN_REQUIRE(ld >= cols, "column_stats: ld < cols");
+    MGN_REQUIRE(ws_bytes >= mgn_column_stats_workspace_bytes(rows, cols), "column_stats: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    int64_t rpb = cdiv64(rows > 0 ? rows : 1, STAT_BLOCKS);
+    if (rpb < 256) rpb = 256;
+    const int nb = (int)cdiv64(rows > 0 ? rows : 1, rpb);
+    float* part = reinterpret_cast<float*>(ws);
+    hipLaunchKernelGGL(colstats_partial, dim3(nb), dim3(256), 0, st, x, rows, (int)cols, ld, rpb, part);
+    MGN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colstats_final, dim3(1), dim3(64), 0, st, (const float*)part, nb, (int)cols, sums);
     MGN_LAUNCH_CHECK();
     return 0;
 }

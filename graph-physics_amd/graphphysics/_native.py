@@ -71,6 +71,8 @@ EXPORTS = {
                                   _vp, _sz, _vp]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgn_column_stats": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _sz, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
     "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
     "mgn_profile_enable": (_i32, [_i32]),
@@ -157,3 +159,19 @@ def mgn_dtype(torch_dtype):
 
 def torch_dtype(mdt):
     return torch.float32 if mdt == MGN_F32 else torch.bfloat16
+
+
+def column_stats(x):
+    """(Σ_rows x, Σ_rows x²) of a 2-D fp32 HIP tensor as two [1, cols] tensors (mgn_column_stats)."""
+    import torch
+
+    require_device(x)
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1:
+        x = x.float().contiguous()
+    rows, cols = x.shape
+    out = torch.empty(2 * cols, dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(int(lib().mgn_column_stats_workspace_bytes(rows, cols)), 4), dtype=torch.uint8,
+                     device=x.device)
+    check(lib().mgn_column_stats(ptr(x), rows, cols, x.stride(0), ptr(out), ptr(ws), ws.numel(),
+                                 stream_ptr(x.device)))
+    return out[:cols].view(1, cols), out[cols:].view(1, cols)

@@ -87,8 +87,13 @@ class Normalizer(nn.Module):
         return normalized_batch_data * self._std_with_epsilon() + self._mean()
 
     def _accumulate(self, d: torch.Tensor):
-        s = torch.sum(d, dim=0, keepdim=True)
-        s2 = torch.sum(d ** 2, dim=0, keepdim=True)
+        if d.is_cuda and d.dim() == 2 and 1 <= d.shape[1] <= 32:
+            from graphphysics import _native as nat  # batch statistics in one native pass
+
+            s, s2 = nat.column_stats(d.float())
+        else:
+            s = torch.sum(d, dim=0, keepdim=True)
+            s2 = torch.sum(d ** 2, dim=0, keepdim=True)
         cnt = torch.full((), float(d.shape[0]), device=d.device)
         if self.process_group is not None:
             import torch.distributed as dist

@@ -167,6 +167,13 @@ int mgn_permute_rows(const void* in, void* out, const int32_t* idx, int64_t rows
 int mgn_segment_sum(const void* src, const int32_t* seg_ptr, int64_t segments, int32_t cols,
                     int32_t dtype, void* out, mgn_stream_t stream);
 
+/* Column sums and sums of squares of a row-major fp32 [rows, cols] matrix (row stride ld), the
+ * batch statistics of Normalizer._accumulate (reference layers.py:333-352): sums[0:cols] = Σ_r x,
+ * sums[cols:2cols] = Σ_r x². cols <= 32. Fixed reduction order (deterministic). */
+size_t mgn_column_stats_workspace_bytes(int64_t rows, int32_t cols);
+int mgn_column_stats(const float* x, int64_t rows, int32_t cols, int64_t ld, float* sums, void* ws,
+                     size_t ws_bytes, mgn_stream_t stream);
+
 /* torch.optim.AdamW semantics (decoupled weight decay p *= 1 - lr*wd, bias-corrected moments,
  * denominator sqrt(v)/sqrt(1-beta2^t) + eps), fp32, over n contiguous elements. */
 int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,

@@ -420,3 +420,21 @@ def test_one_step_mse_matches_reference_path(dtype):
         pred = pred.cpu()
         pred[keep], pr[keep] = y[keep], y[keep]
         assert abs(O.l2_loss(y, pred, x[:, 2]).item() - O.l2_loss(y, pr, x[:, 2]).item()) <= 1e-5
+
+
+def test_column_stats_vs_fp64():
+    """mgn_column_stats (Normalizer batch statistics) vs an fp64 column sum, incl. strided rows."""
+    from graphphysics import _native as nat
+
+    g = torch.Generator().manual_seed(3)
+    for rows, cols in ((1, 3), (777, 11), (88560, 3), (15384, 2)):
+        x = torch.randn(rows, cols, generator=g) * 3 + 1
+        s, s2 = nat.column_stats(x.to(DEV))
+        x64 = x.double()
+        torch.testing.assert_close(s.cpu().double(), x64.sum(0, keepdim=True), rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(s2.cpu().double(), (x64 ** 2).sum(0, keepdim=True), rtol=1e-5, atol=1e-3)
+    wide = torch.randn(100, 40, generator=g).to(DEV)[:, 5:16]  # non-contiguous: row stride 40
+    s, s2 = nat.column_stats(wide)
+    torch.testing.assert_close(s.cpu().double(), wide.cpu().double().sum(0, keepdim=True), rtol=1e-5, atol=1e-4)
+    a, b = nat.column_stats(wide)
+    assert torch.equal(a, s) and torch.equal(b, s2)  # deterministic
