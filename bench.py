@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-mse", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    ap.add_argument("--dp", action="store_true",
+                    help="use the data-parallel step (exchanges + split graph) even on one rank")
     return ap.parse_args()
 
 
@@ -82,8 +84,10 @@ def main():
         a.gpus = world
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+    if world > 1 or a.dp:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
     import __graft_entry__ as ge
 
     if rank == 0:
@@ -116,7 +120,7 @@ def main():
     opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
     sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
     sim.train()
-    step = TrainStep(sim, opt, sched, data, graph=not a.no_graph)
+    step = TrainStep(sim, opt, sched, data, graph=not a.no_graph, data_parallel=(world > 1 or a.dp))
     if step.use_graph:
         step.capture(warmup=max(a.warmup - 1, 1))
         step()  # first replay
@@ -189,7 +193,9 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
         "data": "synthetic: %d jittered copies of the reference in-tree CylinderFlow mesh per GPU, "
                 "random-init weights (seed 0)" % a.batch,
-        "execution": "hipGraph replay of the whole step" if step.use_graph else "eager",
+        "execution": ("eager" if not step.use_graph else
+                      "hipGraph replay of forward+loss+backward; eager statistics/gradient all-reduce + AdamW"
+                      if step.dp else "hipGraph replay of the whole step"),
         "config": {"workload": "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, h, a.batch),
                    "nodes_per_gpu": N, "edges_per_gpu": E, "global_batch": a.batch * world,
                    "parallelism": "dp%d" % world, "graphs_per_sec": round(value * a.batch, 2)},
@@ -205,6 +211,7 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

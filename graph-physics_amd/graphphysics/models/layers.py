@@ -77,6 +77,32 @@ class Normalizer(nn.Module):
         self.register_buffer("_acc_sum_squared",
                              torch.zeros((1, size), dtype=torch.float32, device=device))
         self.process_group = None
+        self._pending = None  # (sum, sum_sq, count) of the global batch, set by set_pending()
+
+    def batch_statistics(self, d: torch.Tensor):
+        """(Σ rows, Σ rows², row count) of one local batch (no exchange)."""
+        if d.is_cuda and d.dim() == 2 and 1 <= d.shape[1] <= 32:
+            from graphphysics import _native as nat  # batch statistics in one native pass
+
+            s, s2 = nat.column_stats(d.float())
+        else:
+            s = torch.sum(d, dim=0, keepdim=True)
+            s2 = torch.sum(d ** 2, dim=0, keepdim=True)
+        return s, s2, torch.full((), float(d.shape[0]), device=d.device)
+
+    def set_pending(self, s, s2, cnt):
+        """Statistics (already summed over ranks) that the next accumulating forward uses instead of
+        computing and exchanging its own: lets a data-parallel step exchange them before a replayed
+        hipGraph. The buffers are static, so a captured forward reads each step's values."""
+        if self._pending is None:
+            self._pending = (s.detach().clone(), s2.detach().clone(), cnt.detach().clone().reshape(()))
+        else:
+            self._pending[0].copy_(s)
+            self._pending[1].copy_(s2)
+            self._pending[2].copy_(cnt.reshape(()))
+
+    def clear_pending(self):
+        self._pending = None
 
     def forward(self, batched_data: torch.Tensor, accumulate: bool = True) -> torch.Tensor:
         if accumulate:
@@ -87,15 +113,11 @@ class Normalizer(nn.Module):
         return normalized_batch_data * self._std_with_epsilon() + self._mean()
 
     def _accumulate(self, d: torch.Tensor):
-        if d.is_cuda and d.dim() == 2 and 1 <= d.shape[1] <= 32:
-            from graphphysics import _native as nat  # batch statistics in one native pass
-
-            s, s2 = nat.column_stats(d.float())
+        if self._pending is not None:
+            s, s2, cnt = self._pending
         else:
-            s = torch.sum(d, dim=0, keepdim=True)
-            s2 = torch.sum(d ** 2, dim=0, keepdim=True)
-        cnt = torch.full((), float(d.shape[0]), device=d.device)
-        if self.process_group is not None:
+            s, s2, cnt = self.batch_statistics(d)
+        if self.process_group is not None and self._pending is None:
             import torch.distributed as dist
 
             packed = torch.cat([s.reshape(-1), s2.reshape(-1), cnt.reshape(1)])

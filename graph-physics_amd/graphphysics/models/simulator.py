@@ -43,6 +43,33 @@ class Simulator(nn.Module):
             if n is not None:
                 n.process_group = group
 
+    def normalizers(self):
+        return [n for n in (self._output_normalizer, self._node_normalizer, self._edge_normalizer)
+                if n is not None]
+
+    @torch.no_grad()
+    def exchange_statistics(self, inputs, group=None):
+        """Data-parallel prologue for a replayed step: the batch statistics of all three normalizers
+        (the same inputs the training forward accumulates) in ONE packed all-reduce over `group`,
+        parked with Normalizer.set_pending() for the next forward. They depend only on the batch, so
+        exchanging them before the (captured) forward is exact."""
+        import torch.distributed as dist
+
+        delta = inputs.y - self._get_pre_target(inputs)
+        nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
+        srcs = [(self._output_normalizer, delta), (self._node_normalizer, nf)]
+        if self._edge_normalizer is not None:
+            srcs.append((self._edge_normalizer, inputs.edge_attr))
+        stats = [n.batch_statistics(d) for n, d in srcs]
+        packed = torch.cat([t.reshape(-1).float() for st in stats for t in st])
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(packed, group=group)
+        o = 0
+        for (n, _), (s, s2, _) in zip(srcs, stats):
+            k = s.numel()
+            n.set_pending(packed[o:o + k].view_as(s), packed[o + k:o + 2 * k].view_as(s2), packed[o + 2 * k])
+            o += 2 * k + 1
+
     def _get_pre_target(self, inputs) -> torch.Tensor:
         return inputs.x[:, self.output_index_start:self.output_index_end]
 

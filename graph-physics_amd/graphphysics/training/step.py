@@ -9,8 +9,12 @@ Captured mode (single process): the whole forward + backward + AdamW launch sequ
 is recorded once into a hipGraph and replayed; per step the host only writes {lr, step} to the
 device and calls replay(), so host/launch overhead disappears. Requires a static batch (the bench's
 resident synthetic meshes, or a training loop that copies each batch into the same buffers).
-Data parallel (process group of >1 rank): eager step with the three exchanges of
-graphphysics.training.distributed (normalizer statistics, global masked-node count, gradients).
+Data parallel (process group of >1 rank), captured: the three exchanges of
+graphphysics.training.distributed stay outside the graph — the normalizer batch statistics depend
+only on the batch, so Simulator.exchange_statistics() sums them over ranks (one packed all-reduce)
+before the replay; the global masked-node count is fixed per batch; the replay covers forward,
+loss and backward; then ONE all-reduce of the flat gradient buffer and the AdamW launch.
+`graph=False`: the same exchanges, fully eager.
 """
 import torch
 import torch.distributed as dist
@@ -22,31 +26,38 @@ from graphphysics.utils.nodetype import NodeType
 
 class TrainStep:
     def __init__(self, sim, opt, sched, batch, masks=(NodeType.NORMAL, NodeType.OUTFLOW), graph=True,
-                 group=None):
+                 group=None, data_parallel=None):
         self.sim, self.opt, self.sched, self.batch = sim, opt, sched, batch
         self.masks = list(masks)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        # data_parallel=True forces the exchanging step at any world size (tests run it on 1 rank)
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
         self.node_type = batch.x[:, sim.node_type_index]
         self.params = [p for p in sim.parameters() if p.requires_grad]
-        self.use_graph = graph and self.world == 1
+        self.use_graph = graph
         self.graph = None
         self.static_loss = None
         self._count = None
-        if self.world > 1:
+        if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
 
     def _loss(self):
         net, tdn, _ = self.sim(self.batch)
         return masked_mse(tdn, net, self.node_type, self.masks, count=self._count)
 
+    def _prologue(self):
+        if self.dp:
+            if self._count is None:
+                self._count = global_mask_count(self.node_type, self.masks, self.group)
+            self.sim.exchange_statistics(self.batch, self.group)
+
     def eager(self):
         self.opt.zero_grad(set_to_none=True)
-        if self.world > 1 and self._count is None:
-            self._count = global_mask_count(self.node_type, self.masks, self.group)
+        self._prologue()
         loss = self._loss()
         loss.backward()
-        if self.world > 1:
+        if self.dp:
             allreduce_gradients(self.params, self.group)
         self.opt.step()
         self.sched.step()
@@ -65,11 +76,13 @@ class TrainStep:
         self.opt.zero_grad(set_to_none=True)
         if on_record is not None:
             on_record()
+        self._prologue()  # pending statistics exist before recording (the graph reads their buffers)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._loss()
             loss.backward()
-            self.opt.launch()
+            if not self.dp:
+                self.opt.launch()
         self.graph, self.static_loss = g, loss
         return self
 
@@ -79,6 +92,12 @@ class TrainStep:
         if self.graph is None:
             self.capture()
         self.opt.stage()
-        self.graph.replay()
+        if self.dp:
+            self._prologue()
+            self.graph.replay()
+            allreduce_gradients(self.params, self.group)
+            self.opt.launch()
+        else:
+            self.graph.replay()
         self.sched.step()
         return self.static_loss

@@ -35,13 +35,15 @@ def _shard(b, rank, world):
             "edge_attr": b["edge_attr"][keep]}
 
 
-def _step(sim, d, group):
+def _step(sim, d, group, prologue=False):
     from graphphysics.training.distributed import allreduce_gradients, global_masked_mse
     from graphphysics.utils.data import Data
     from graphphysics.utils.loss import masked_mse
     from graphphysics.utils.nodetype import NodeType
 
     data = Data(**{k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in d.items()})
+    if prologue:  # the captured step's form: statistics exchanged before the forward
+        sim.exchange_statistics(data, group)
     net, tdn, _ = sim(data)
     masks = [NodeType.NORMAL, NodeType.OUTFLOW]
     loss = (global_masked_mse(tdn, net, data.x[:, 2], masks, group) if group is not None
@@ -52,7 +54,7 @@ def _step(sim, d, group):
     return loss
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, prologue=False):
     import sys
 
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
@@ -66,7 +68,7 @@ def _worker(rank, world, port, out):
     b = meshes.cylinder_batch(4, jitter=0.01)
     sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
     sim.set_process_group(dist.group.WORLD)
-    loss = _step(sim, _shard(b, rank, world), dist.group.WORLD)
+    loss = _step(sim, _shard(b, rank, world), dist.group.WORLD, prologue)
     dist.all_reduce(loss.detach())
     res = {"loss": loss.item(), "acc": sim._node_normalizer._acc_sum.clone(),
            "cnt": sim._edge_normalizer._acc_count.item(),
@@ -75,13 +77,15 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_rank_step_equals_single_process_step():
+@pytest.mark.parametrize("prologue", [False, True])
+def test_two_rank_step_equals_single_process_step(prologue):
     from graphphysics.models.simulator import Simulator
     from graphphysics.utils import meshes
 
     port = 29500 + os.getpid() % 1000
     with tempfile.TemporaryDirectory() as out:
-        mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(2, port + int(prologue), out, prologue), nprocs=2, join=True,
+                           start_method="spawn")
         r = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(2)]
     b = meshes.cylinder_batch(4, jitter=0.01)
     sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")

@@ -438,3 +438,42 @@ def test_column_stats_vs_fp64():
     torch.testing.assert_close(s.cpu().double(), wide.cpu().double().sum(0, keepdim=True), rtol=1e-5, atol=1e-4)
     a, b = nat.column_stats(wide)
     assert torch.equal(a, s) and torch.equal(b, s2)  # deterministic
+
+
+def test_captured_data_parallel_step_matches_captured_step():
+    """The N>1 bench step (statistics exchanged before a replayed forward+backward graph, eager
+    gradient all-reduce + AdamW) run on a 1-rank RCCL group equals the single-process captured step."""
+    import torch.distributed as dist
+
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.optim import FusedAdamW
+    from graphphysics.training.step import TrainStep
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+    from graphphysics.utils.scheduler import CosineWarmupScheduler
+
+    b = meshes.cylinder_batch(2, jitter=0.01)
+    batch = Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})
+
+    def run(dp):
+        torch.manual_seed(0)
+        model = EncodeProcessDecode(3, 11, 3, 2, 32, compute_dtype=torch.float32)
+        sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, model, DEV).to(DEV)
+        opt = FusedAdamW(sim.parameters(), lr=1e-3, weight_decay=1e-4)
+        sched = CosineWarmupScheduler(opt, warmup=5, max_iters=100)
+        step = TrainStep(sim, opt, sched, batch, graph=True, data_parallel=dp)
+        losses = [float(step().detach()) for _ in range(4)]
+        return losses, [p.detach().clone() for p in sim.parameters()]
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29700 + os.getpid() % 200))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        l_dp, p_dp = run(True)
+    finally:
+        dist.destroy_process_group()
+    l_1, p_1 = run(False)
+    np.testing.assert_allclose(l_dp, l_1, rtol=1e-6)
+    for a, c in zip(p_dp, p_1):
+        torch.testing.assert_close(a, c, rtol=1e-6, atol=1e-7)
