@@ -71,29 +71,36 @@ __device__ __forceinline__ f4 ld4bf(const __bf16* p) {
 // one row (fwd pack) / 4 consecutive n of one column (transposed pack) are 8 contiguous bytes.
 __device__ __forceinline__ void stage_weights(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
                                               bool transposed) {
-    constexpr int PER = 4 * LFR * 64 * 2 / (NW * 64);  // 64 8-byte pieces per thread, all in flight
-    constexpr int BATCH = 32;
+    // Linear walk over the packed 16x16x32 fragments (16-byte loads, fully coalesced): a source
+    // chunk is 8 consecutive reduction indices (k of the fwd pack, n of the transposed pack) of one
+    // A-operand row a; its two 4-element halves land in two (k-step, lane half, element group)
+    // slots of the chain image. Per layer 8 row tiles x 4 k-steps x 64 lanes = 2048 chunks.
+    constexpr int PER = 4 * 2048 / (NW * 64);  // 32 chunks per thread, all in flight
+    u32x4 v[PER];
 #pragma unroll
-    for (int b0 = 0; b0 < PER; b0 += BATCH) {
-        u32x2 v[BATCH];
-        int dst[BATCH];
+    for (int u = 0; u < PER; ++u) {
+        const int it = threadIdx.x + u * NW * 64;
+        const int l = it >> 11, c = it & 2047;
+        const int tile = c >> 6, lane16 = c & 63;  // tile = rt*4 + ks (rt: 16-row tile of a)
+        const int rt = tile >> 2, ks = tile & 3;
+        const int ksl = transposed ? 4 : wks[l];
+        v[u] = *reinterpret_cast<const u32x4*>(pack + woff[l] + ((int64_t)(rt * ksl + ks) * 64 + lane16) * 8);
+    }
 #pragma unroll
-        for (int u = 0; u < BATCH; ++u) {
-            const int it = threadIdx.x + (b0 + u) * NW * 64;
-            const int jg = it & 1, lane = (it >> 1) & 63, fr = it >> 7;
-            const int l = fr >> 5, t = (fr >> 3) & 3, S = fr & 7;
-            const int a = 32 * t + (lane & 31);               // row of the A operand (out feature)
-            const int b = 16 * S + 8 * jg + 4 * (lane >> 5);  // first of 4 reduction indices
-            int64_t src;
-            if (!transposed)  // fwd pack: tile nt*KS + ks, lane (n&15) + 16((k>>3)&3), v = k&7
-                src = woff[l] + ((int64_t)((a >> 4) * wks[l] + (b >> 5)) * 64 + ((b >> 3) & 3) * 16 + (a & 15)) * 8 + (b & 7);
-            else              // transposed pack: tile kt*NS + ns (NS = 4), lane (k&15) + 16((n>>3)&3), v = n&7
-                src = woff[l] + ((int64_t)((a >> 4) * 4 + (b >> 5)) * 64 + (a & 15) + 16 * ((b >> 3) & 3)) * 8 + (b & 7);
-            v[u] = *reinterpret_cast<const u32x2*>(pack + src);
-            dst[u] = (fr * 64 + lane) * 8 + jg * 4;
+    for (int u = 0; u < PER; ++u) {
+        const int it = threadIdx.x + u * NW * 64;
+        const int l = it >> 11, c = it & 2047;
+        const int tile = c >> 6, lane16 = c & 63;
+        const int rt = tile >> 2, ks = tile & 3;
+        const int a = rt * 16 + (lane16 & 15);             // A-operand row
+        const int t = a >> 5, r = a & 31;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int b = 32 * ks + 8 * (lane16 >> 4) + 4 * half;  // first of 4 reduction indices
+            const int S = b >> 4, jg = (b >> 3) & 1, h = (b >> 2) & 1;
+            const u32x2 w = {v[u][2 * half], v[u][2 * half + 1]};
+            *reinterpret_cast<u32x2*>(W + ((size_t)((l * 4 + t) * 8 + S) * 64 + r + 32 * h) * 8 + jg * 4) = w;
         }
-#pragma unroll
-        for (int u = 0; u < BATCH; ++u) *reinterpret_cast<u32x2*>(W + dst[u]) = v[u];
     }
 }
 
@@ -275,23 +282,24 @@ __global__ __launch_bounds__(NW * 64) void chain_fwd_kernel(ChainFwdArgs a) {
     float* vec = reinterpret_cast<float*>(smem + LDS_W);  // bias[4][H], scale[H]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
-    stage_weights(W, a.wpack, a.woff, a.wks, false);
-    for (int i = threadIdx.x; i < 5 * H; i += NW * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
-    __syncthreads();
-
     const int m = lane & 31, h = lane >> 5;
     const int64_t stride = (int64_t)gridDim.x * NW;
     int64_t tile = (int64_t)blockIdx.x * NW + wave;
-    if (tile >= a.ntiles) return;
+    const int64_t last = a.ntiles - 1;  // prefetch targets past the end are clamped (unconditional loads)
+    // the first tile's inputs are in flight while the weights are staged
     FwdIn nxt;
     int di, dj;
-    fwd_idx(a, tile, lane, di, dj);
-    fwd_load(nxt, a, tile, lane);
+    fwd_idx(a, min(tile, last), lane, di, dj);
+    fwd_load(nxt, a, min(tile, last), lane);
+    stage_weights(W, a.wpack, a.woff, a.wks, false);
+    for (int i = threadIdx.x; i < 5 * H; i += NW * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
+    __syncthreads();
+    if (a.ablate & 16) return;  // diagnostics: staging only
+    if (tile >= a.ntiles) return;
 #pragma unroll
     for (int S = 0; S < 8; ++S) pin(nxt.eb[S]);
     pin(di);
     pin(dj);
-    const int64_t last = a.ntiles - 1;  // prefetch targets past the end are clamped (unconditional loads)
     for (; tile < a.ntiles; tile += stride) {
         const FwdIn in = nxt;
         FwdProj pr;
@@ -402,21 +410,24 @@ __global__ __launch_bounds__(NW * 64) void chain_bwd_kernel(ChainBwdArgs a) {
     float* vec = reinterpret_cast<float*>(smem + LDS_W);  // scale[H], then dscale reduction [NW][H]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
-    stage_weights(W, a.wtpack, a.woff, a.wks, true);
-    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
-    __syncthreads();
-
     const int m = lane & 31, h = lane >> 5;
     const int64_t stride = (int64_t)gridDim.x * NW;
     int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t last = a.ntiles - 1;  // prefetch targets past the end are clamped (unconditional loads)
+    // the first tile's inputs are in flight while the weights are staged
+    const int gi0 = bwd_idx(a, min(tile, last), lane);
+    stage_weights(W, a.wtpack, a.woff, a.wks, true);
+    BwdIn nxt;
+    bwd_load(nxt, a, min(tile, last), gi0, lane);
+    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
+    __syncthreads();
+    if (a.ablate & 16) return;  // diagnostics: staging only
+
     f4 dsc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) dsc[q] = f4{0.f, 0.f, 0.f, 0.f};
-    BwdIn nxt;
-    const int64_t last = a.ntiles - 1;  // prefetch targets past the end are clamped (unconditional loads)
     int ngi = 0;
     if (tile < a.ntiles) {
-        bwd_load(nxt, a, tile, bwd_idx(a, tile, lane), lane);
         ngi = bwd_idx(a, min(tile + stride, last), lane);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {

@@ -1,5 +1,5 @@
 """Diagnostic: time the chained edge-MLP kernels (forward + backward) with phases removed
-(MGN_ABLATE bits: 1 input loads from HBM, 2 R8 saves, 4 MFMA, 8 row-major stores). Cfg B block,
+(MGN_ABLATE bits: 1 input loads from HBM, 2 R8 saves, 4 MFMA, 8 row-major stores, 16 exit after weight staging). Cfg B block,
 bf16 h=128. Results are wrong when a bit is set; timing only."""
 import os
 import sys
