@@ -20,7 +20,8 @@ struct ChainFwdArgs {
     __bf16* act8;               // R8 saved inputs of layers 1..3
     int64_t act_off[4];
     unsigned long long* mask;   // [3][ntiles*64]: lane-owned ReLU bits
-    int64_t mask_stride;
+    unsigned* mask32;           // 16-row variant: [3][ntiles16*64] 32-bit lane words
+    int64_t mask_stride;        // 64-bit words per layer
     int32_t ablate;             // diagnostics only (env MGN_ABLATE): 1 loads, 2 R8 saves, 4 MFMA, 8 row stores
 };
 
@@ -33,6 +34,7 @@ struct ChainBwdArgs {
     const float* scale;
     float dinv;
     const unsigned long long* mask;
+    const unsigned* mask32;
     int64_t mask_stride;
     const __bf16* wtpack;       // transposed 16x16x32 fragments of the 4 layers
     int64_t woff[4];
@@ -54,3 +56,11 @@ int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, co
                         const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
                         hipStream_t st);
 size_t chain_lds_bytes();
+// 16-row variant (mgn_chain16.hip): same contracts, 16x16x32 tiles, two waves per SIMD
+int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
+int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
+                          const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
+                          hipStream_t st);
+// which chained variant block forward/backward use (read once; env MGN_CHAIN=32 or 16)
+int chain_variant();

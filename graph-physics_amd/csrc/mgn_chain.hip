@@ -619,7 +619,7 @@ int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const
     a.scale = m->scale;
     a.dinv = (float)(1.0 / sqrt((double)H));
     a.M = M;
-    a.ntiles = cdiv64(M, TR);
+    a.ntiles = rows_pad(M) / TR;  // every padded row: R8 saves and masks cover rows_pad(M)
     a.out = reinterpret_cast<__bf16*>(out);
     a.z_save = reinterpret_cast<__bf16*>(sv->z);
     a.rden_save = sv->rden;
@@ -653,7 +653,7 @@ int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, co
     a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
     layer_offsets(m, a.woff, a.wks);
     a.M = M;
-    a.ntiles = cdiv64(M, TR);
+    a.ntiles = rows_pad(M) / TR;  // every padded row: R8 saves and masks cover rows_pad(M)
     a.dz8 = reinterpret_cast<__bf16*>(dz8);
     a.RP = rows_pad(M);
     a.dscale_part = dscale_part;
@@ -672,3 +672,14 @@ int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, co
 }
 
 size_t chain_lds_bytes() { return LDS_TOTAL; }
+
+// 16 (default): mgn_chain16.hip, 16-row tiles, two waves per SIMD. 32: the 32x32x16 kernels above
+// (one wave per SIMD), kept for A/B measurement. Read once: forward and backward must agree on the
+// ReLU-mask layout.
+int chain_variant() {
+    static const int v = [] {
+        const char* e = getenv("MGN_CHAIN");
+        return e && atoi(e) == 32 ? 32 : 16;
+    }();
+    return v;
+}

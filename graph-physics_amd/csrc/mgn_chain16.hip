@@ -1,0 +1,550 @@
+// Register-chained edge-MLP kernels on 16-row tiles (v_mfma_f32_16x16x32_bf16), bf16, h=128.
+//
+// Same structure as mgn_chain.hip (one wave runs the whole 4-Linear chain of its edges, weights
+// resident in LDS, accumulators chained as the next layer's B operand), on 16x16x32 tiles: a wave
+// owns 16 edges, its accumulator is 8 f32x4 (32 VGPRs) instead of 64, so TWO waves fit per SIMD
+// (8 waves per workgroup share one 128 KiB weight image) and one wave's epilogue VALU overlaps the
+// other's MFMAs and memory traffic.
+//
+// Lane l: edge m = l&15, group g = l>>4. Accumulator tile t (16 features): lane holds features
+// 16t + 4g + r, r = 0..3. B operand k-step s (32 features): element j of lane group g is feature
+// 32s + 16(j>>2) + 4g + (j&3) = accumulator (t = 2s + (j>>2), r = j&3): the next layer's operand
+// is the accumulator with no data movement, given weights staged in that permuted k order.
+// ReLU masks: 32 bits per lane (bit 4t + r) per tile and layer; the backward has the same map.
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+#include "mgn_chain.h"
+
+namespace {
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int H = 128;
+constexpr int TR = 16;                 // edges per wave tile
+constexpr int NW = 8;                  // waves per workgroup (2 per SIMD)
+constexpr int FRAG = 512;              // bf16 per 16x16x32 operand fragment (64 lanes x 8)
+constexpr int LFR = 32;                // fragments per layer: 8 out-tiles x 4 k-steps
+constexpr int SLD = H + 8;             // scratch row stride (bf16)
+constexpr int SROWS = 8;               // scratch rows (one R8 octet per pass)
+constexpr size_t LDS_W = (size_t)4 * LFR * FRAG * 2;   // 128 KiB
+constexpr size_t LDS_V = (size_t)5 * H * 4;             // 4 bias vectors + scale / dscale reduction
+constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose scratch
+constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
+constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
+
+__device__ __forceinline__ f4 mfma16(const bf16x8& a, const bf16x8& b, const f4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <class T>
+__device__ __forceinline__ void pin(const T& v) { asm volatile("" ::"v"(v)); }
+
+__device__ __forceinline__ f4 bf4(u32x2 v) {
+    const bf16x4 b = __builtin_bit_cast(bf16x4, v);
+    return f4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
+
+// sum over the 16 lanes of a DPP row (lanes 16g .. 16g+15), result in every lane of the row:
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+__device__ __forceinline__ int64_t clamp_row(int64_t row, int64_t M) { return row < M ? row : M - 1; }
+
+// w = 2w + (v > 0) (see mgn_chain.hip)
+__device__ __forceinline__ unsigned push_bit(unsigned w, float v) {
+    unsigned r;
+    asm("v_cmp_lt_f32 vcc, 0, %2\n\tv_addc_co_u32 %0, vcc, %1, %1, vcc" : "=v"(r) : "v"(w), "v"(v) : "vcc");
+    return r;
+}
+__device__ __forceinline__ int bit_sel(unsigned w, int k) { return (int)(w << k) >> 31; }
+
+// Weight image: fragment (l, t, s) lane (r, g) element j = A_l[16t + r][32s + 16(j>>2) + 4g + (j&3)]
+// (A = W forward, Wᵀ backward). Linear walk over libmgn's 16x16x32 packs (16-byte coalesced loads):
+// a source chunk holds 8 consecutive reduction indices 32s + 8q .. +7 of one row; its halves go to
+// lane groups g = 2(q&1) + half, element group jg = q>>1.
+__device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
+                                        bool transposed) {
+    constexpr int PER = 4 * 2048 / (NW * 64);  // 16 chunks per thread
+    u32x4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int it = threadIdx.x + u * NW * 64;
+        const int l = it >> 11, c = it & 2047;
+        const int tile = c >> 6, lane16 = c & 63;
+        const int rt = tile >> 2, ks = tile & 3;
+        const int ksl = transposed ? 4 : wks[l];
+        v[u] = *reinterpret_cast<const u32x4*>(pack + woff[l] + ((int64_t)(rt * ksl + ks) * 64 + lane16) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int it = threadIdx.x + u * NW * 64;
+        const int l = it >> 11, c = it & 2047;
+        const int tile = c >> 6, lane16 = c & 63;
+        const int rt = tile >> 2, ks = tile & 3;
+        const int r = lane16 & 15, q = lane16 >> 4;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int g = (2 * q + half) & 3, jg = q >> 1;
+            const u32x2 w = {v[u][2 * half], v[u][2 * half + 1]};
+            *reinterpret_cast<u32x2*>(W + ((size_t)((l * 8 + rt) * 4 + ks) * 64 + r + 16 * g) * 8 + jg * 4) = w;
+        }
+    }
+}
+
+__device__ __forceinline__ bf16x8 wfrag(const __bf16* W, int l, int t, int s, int lane) {
+    return *reinterpret_cast<const bf16x8*>(W + ((size_t)((l * 8 + t) * 4 + s) * 64 + lane) * 8);
+}
+
+__device__ __forceinline__ void gemm16(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    // one k-step's 8 fragments in flight at a time (the other wave on the SIMD covers the LDS
+    // latency); without the fence the scheduler hoists all 32 reads and the backward spills
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, l, t, s, lane), B[s], acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__device__ __forceinline__ void to_operand(const f4 (&v)[8], bf16x8 (&B)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) B[s][j] = (__bf16)v[2 * s + (j >> 2)][j & 3];
+}
+
+// write this lane's 32 values of row m (&7) of one octet into the scratch
+__device__ __forceinline__ void scr_write(const f4 (&v)[8], __bf16* scr, int lane) {
+    const int m = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const bf16x4 w = {(__bf16)v[t][0], (__bf16)v[t][1], (__bf16)v[t][2], (__bf16)v[t][3]};
+        *reinterpret_cast<bf16x4*>(scr + (m & 7) * SLD + 16 * t + 4 * g) = w;
+    }
+}
+
+// The wave's 16x128 tile (D layout) as bf16 into an R8 matrix [RP][128], octets 2*tile, 2*tile+1.
+__device__ __forceinline__ void store_r8(const f4 (&v)[8], __bf16* scr, __bf16* dst, int64_t tile, int lane) {
+    const int m = lane & 15;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        if ((m >> 3) == u) scr_write(v, scr, lane);
+        lds_fence();
+        // lane = column pair: 8 rows x 4 B -> 2 R8 chunks (32 contiguous bytes per lane)
+        u32x2 rv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rv[q][0] = *reinterpret_cast<const unsigned*>(scr + q * SLD + 2 * lane);
+        bf16x8 c0, c1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bf16x2 p = __builtin_bit_cast(bf16x2, rv[q][0]);
+            c0[q] = p[0];
+            c1[q] = p[1];
+        }
+        __bf16* p = dst + (((int64_t)tile * 2 + u) * H + 2 * lane) * 8;
+        *reinterpret_cast<bf16x8*>(p) = c0;
+        *reinterpret_cast<bf16x8*>(p + 8) = c1;
+        lds_fence();
+    }
+}
+
+// The wave's tile as bf16 rows of a row-major [M][128] matrix (rows >= M skipped), 16-byte stores.
+__device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16* dst, int64_t tile, int64_t M,
+                                           int lane) {
+    const int m = lane & 15;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        if ((m >> 3) == u) scr_write(v, scr, lane);
+        lds_fence();
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int rr = 4 * p + (lane >> 4), c = (lane & 15) * 8;
+            const u32x4 w = *reinterpret_cast<const u32x4*>(scr + rr * SLD + c);
+            const int64_t row = tile * TR + 8 * u + rr;
+            if (row < M) *reinterpret_cast<u32x4*>(dst + row * H + c) = w;
+        }
+        lds_fence();
+    }
+}
+
+int chain16_grid(int64_t ntiles) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    const int64_t groups = cdiv64(ntiles, NW);
+    return (int)(groups < cus ? groups : cus);
+}
+
+void layer_offsets(const mgn_mlp* m, int64_t* woff, int* wks) {
+    int64_t o = 0;
+    for (int l = 0; l < 4; ++l) {
+        int n, k;
+        mlp_layer_shape(*m, l, &n, &k);
+        woff[l] = o;
+        wks[l] = cdiv(k, 32);
+        o += linear_pack_elems(n, k, MGN_BF16);
+    }
+}
+
+// ------------------------------------------------------------------------------------ forward
+struct In16 {
+    bf16x8 eb[4];  // layer-0 B operand = e[row][32s + 16(j>>2) + 4g + (j&3)]; also the residual
+};
+
+__device__ __forceinline__ void load_e(In16& in, const ChainFwdArgs& a, int64_t tile, int lane) {
+    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
+    const __bf16* e = a.e + row * H + 4 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(e + 32 * s);
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(e + 32 * s + 16);
+        const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+        in.eb[s] = __builtin_bit_cast(bf16x8, w);
+    }
+}
+
+__device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, int lane, int& di, int& dj) {
+    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
+    di = a.proj_i[row];
+    dj = a.proj_j[row];
+}
+
+__global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // bias[4][H], scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    const int m = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t last = a.ntiles - 1;
+    In16 nxt;
+    int di, dj;
+    load_idx(a, min(tile, last), lane, di, dj);
+    load_e(nxt, a, min(tile, last), lane);
+    stage16(W, a.wpack, a.woff, a.wks, false);
+    for (int i = threadIdx.x; i < 5 * H; i += NW * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
+    __syncthreads();
+    if (tile >= a.ntiles) return;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
+    pin(di);
+    pin(dj);
+    for (; tile < a.ntiles; tile += stride) {
+        const In16 in = nxt;
+        // node projections of this tile (b0 folded into P_i); the layer-0 GEMM covers their latency
+        f4 pi[8], pj[8];
+        {
+            const float* p0 = a.proj + (int64_t)di * (2 * H) + 4 * g;
+            const float* p1 = a.proj + (int64_t)dj * (2 * H) + H + 4 * g;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                pi[t] = *reinterpret_cast<const f4*>(p0 + 16 * t);
+                pj[t] = *reinterpret_cast<const f4*>(p1 + 16 * t);
+            }
+        }
+        int ndi, ndj;
+        load_idx(a, min(tile + stride, last), lane, ndi, ndj);
+        load_e(nxt, a, min(tile + stride, last), lane);
+        const int64_t row = tile * TR + m;
+        f4 acc[8];
+        bf16x8 B[4];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            gemm16(acc, W, l, l == 0 ? in.eb : B, lane);
+            unsigned bits = 0u;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f4 b = l == 0 ? pi[t] + pj[t] : *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = fmaxf(acc[t][r] + b[r], 0.f);
+                    acc[t][r] = v;
+                    bits = push_bit(bits, v);
+                }
+            }
+            to_operand(acc, B);
+            a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
+            store_r8(acc, scr, a.act8 + a.act_off[l + 1], tile, lane);
+        }
+        // layer 3 + RMSNorm + residual
+        gemm16(acc, W, 3, B, lane);
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float z = acc[t][r] + b[r];
+                acc[t][r] = z;
+                ss = fmaf(z, z, ss);
+            }
+        }
+        ss += __shfl_xor(ss, 16);
+        ss += __shfl_xor(ss, 32);
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        const float rq = __builtin_amdgcn_rcpf(q);  // bf16 outputs: z·(1/q) is within 2 fp32 ulp of z/q
+        if (g == 0 && row < a.M) a.rden_save[row] = q;
+        store_rows(acc, scr, a.z_save, tile, a.M, lane);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[t][r] = fmaf(s[r], acc[t][r] * rq, (float)in.eb[t >> 1][4 * (t & 1) + r]);
+        }
+        store_rows(acc, scr, a.out, tile, a.M, lane);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
+        pin(ndi);
+        pin(ndj);
+        di = ndi;
+        dj = ndj;
+    }
+}
+
+// ------------------------------------------------------------------------------------ backward
+struct BIn16 {  // raw bf16: features 16t + 4g .. +3
+    u32x2 d[8];     // de_out[row]
+    u32x2 ga[8];    // d_aggr[dst(row)]
+    u32x2 z[8];
+    float q;
+    unsigned mask[3];
+};
+
+__device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
+    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
+    const int off = 4 * (lane >> 4);
+    const __bf16* d = a.dout + row * H + off;
+    const __bf16* gp = a.gath + (int64_t)gi * H + off;
+    const __bf16* z = a.z_save + row * H + off;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        in.d[t] = *reinterpret_cast<const u32x2*>(d + 16 * t);
+        in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+        in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
+    }
+    in.q = a.rden_save[row];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) in.mask[l] = a.mask32[l * a.mask_stride * 2 + tile * 64 + lane];
+}
+
+__device__ __forceinline__ int bidx(const ChainBwdArgs& a, int64_t tile, int lane) {
+    return a.gath_idx[clamp_row(tile * TR + (lane & 15), a.M)];
+}
+
+template <class S>
+__device__ __forceinline__ void pin_in(const S& in) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        pin(in.d[t]);
+        pin(in.ga[t]);
+        pin(in.z[t]);
+    }
+    pin(in.q);
+#pragma unroll
+    for (int l = 0; l < 3; ++l) pin(in.mask[l]);
+}
+
+__global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
+    const int m = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t last = a.ntiles - 1;
+    const int gi0 = bidx(a, min(tile, last), lane);
+    stage16(W, a.wtpack, a.woff, a.wks, true);
+    BIn16 nxt;
+    bload(nxt, a, min(tile, last), gi0, lane);
+    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
+    __syncthreads();
+    // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
+    // over the tile's 16 edges, then the 4 lane-group leaders add their features; fixed order)
+    for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
+    int ngi = 0;
+    if (tile < a.ntiles) {
+        ngi = bidx(a, min(tile + stride, last), lane);
+        pin_in(nxt);
+        pin(ngi);
+    }
+    for (; tile < a.ntiles; tile += stride) {
+        const int64_t row = tile * TR + m;
+        const bool ok = row < a.M;
+        // RMSNorm backward (layers.py:59-74) from the prefetched tile
+        f4 acc[8];
+        float dot = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 dy = bf4(nxt.d[t]) + bf4(nxt.ga[t]);
+            const f4 z = bf4(nxt.z[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            acc[t] = dy;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dot = fmaf(sc[r] * dy[r], z[r], dot);
+        }
+        dot += __shfl_xor(dot, 16);
+        dot += __shfl_xor(dot, 32);
+        const float qd = nxt.q;
+        const float rq = __builtin_amdgcn_rcpf(qd);
+        const float rms = qd - RMS_EPS;
+        const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 z = bf4(nxt.z[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            f4 ds;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dy = acc[t][r];
+                acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
+                ds[r] = row16_sum(ok ? dy * z[r] * rq : 0.f);
+            }
+            if (m == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * t + 4 * g) += ds;
+        }
+        unsigned mcur[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
+        bload(nxt, a, min(tile + stride, last), ngi, lane);
+        const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
+        bf16x8 B[4];
+        to_operand(acc, B);
+        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
+        // layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_l > 0]
+        u32x2 dre[8];  // de_out of this tile again (cache-hot), for the layer-0 residual
+#pragma unroll
+        for (int l = 3; l >= 1; --l) {
+            if (l == 1) {
+                const __bf16* d = a.dout + clamp_row(row, a.M) * H + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) dre[t] = *reinterpret_cast<const u32x2*>(d + 16 * t);
+            }
+            gemm16(acc, W, l, B, lane);
+            const unsigned bw = mcur[l - 1];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[t][r] = __int_as_float(__float_as_int(acc[t][r]) & bit_sel(bw, 4 * t + r));
+            to_operand(acc, B);
+            store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
+            if (l == 1) store_rows(acc, scr, a.dz0, tile, a.M, lane);
+        }
+        // layer 0, e block: de = de_out + dZ0 · W0a
+        gemm16(acc, W, 0, B, lane);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += bf4(dre[t]);
+        store_rows(acc, scr, a.de, tile, a.M, lane);
+        pin_in(nxt);
+        pin(ngi2);
+        ngi = ngi2;
+    }
+    // dscale partials of the workgroup: the waves' rows in wave order
+    __syncthreads();
+    if (threadIdx.x < H) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s += red[w * H + threadIdx.x];
+        a.dscale_part[(int64_t)blockIdx.x * H + threadIdx.x] = s;
+    }
+}
+
+int set_lds_once(const void* fn, size_t bytes) {
+    static std::mutex mu;
+    static bool done[2] = {false, false};
+    std::lock_guard<std::mutex> lk(mu);
+    const int slot = fn == (const void*)chain16_fwd_kernel ? 0 : 1;
+    if (done[slot]) return 0;
+    MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    done[slot] = true;
+    return 0;
+}
+
+}  // namespace
+
+int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st) {
+    ChainFwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.e = reinterpret_cast<const __bf16*>(e);
+    a.proj = proj;
+    a.proj_i = pi;
+    a.proj_j = pj;
+    a.wpack = reinterpret_cast<const __bf16*>(m->wpack);
+    layer_offsets(m, a.woff, a.wks);
+    for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;  // every padded row: R8 saves and masks cover rows_pad(M)
+    a.out = reinterpret_cast<__bf16*>(out);
+    a.z_save = reinterpret_cast<__bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.act8 = reinterpret_cast<__bf16*>(sv->act);
+    for (int l = 0; l < 4; ++l) a.act_off[l] = act_off(*m, M, l, 1);
+    a.mask32 = reinterpret_cast<unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    if (a.ntiles == 0) return 0;
+    if (int e2 = set_lds_once((const void*)chain16_fwd_kernel, LDS_TOTAL)) return e2;
+    ProfScope ps(PROF_FWD_EDGE, st);
+    hipLaunchKernelGGL(chain16_fwd_kernel, dim3(chain16_grid(a.ntiles)), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
+                          const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
+                          hipStream_t st) {
+    ChainBwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dout = reinterpret_cast<const __bf16*>(dout);
+    a.gath = reinterpret_cast<const __bf16*>(gath);
+    a.gath_idx = gath_idx;
+    a.z_save = reinterpret_cast<const __bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
+    layer_offsets(m, a.woff, a.wks);
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;  // every padded row: R8 saves and masks cover rows_pad(M)
+    a.dz8 = reinterpret_cast<__bf16*>(dz8);
+    a.RP = rows_pad(M);
+    a.dscale_part = dscale_part;
+    a.de = reinterpret_cast<__bf16*>(de);
+    a.dz0 = reinterpret_cast<__bf16*>(dz0);
+    *nparts = 0;
+    if (a.ntiles == 0) return 0;
+    if (int e2 = set_lds_once((const void*)chain16_bwd_kernel, LDS_TOTAL)) return e2;
+    const int grid = chain16_grid(a.ntiles);
+    *nparts = grid;
+    ProfScope ps(PROF_BWD_EDGE, st);
+    hipLaunchKernelGGL(chain16_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}

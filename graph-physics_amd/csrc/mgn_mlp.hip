@@ -1741,8 +1741,8 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     ein.proj_i = t->csc_dst;
     ein.proj_j = t->csc_src;
     if (chain) {
-        if (int r = chain_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st))
-            return r;
+        auto fwd = chain_variant() == 16 ? chain16_edge_forward : chain_edge_forward;
+        if (int r = fwd(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st)) return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
                                    nullptr, nullptr, st)) {
         return r;
@@ -1836,9 +1836,8 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     oe.o1 = de;
     oe.o2 = dz0;
     if (chain_eligible(edge)) {
-        if (int r = chain_edge_backward(edge, E, &saved->edge, de_out, d_aggr, t->csc_dst, dz8, dsp, &ntiles, de, dz0,
-                                        st))
-            return r;
+        auto bwd = chain_variant() == 16 ? chain16_edge_backward : chain_edge_backward;
+        if (int r = bwd(edge, E, &saved->edge, de_out, d_aggr, t->csc_dst, dz8, dsp, &ntiles, de, dz0, st)) return r;
     } else if (E > 0) {
         if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, dz8, dsp, st)) return r;
     }
