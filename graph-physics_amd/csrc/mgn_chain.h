@@ -48,7 +48,56 @@ struct ChainBwdArgs {
     int32_t ablate;             // as ChainFwdArgs
 };
 
+// Node MLP (16-row chained kernels): in = [x ‖ aggr], aggr[v] = Σ_{k: dst(k)=v} s_e ⊙ z_k / q_k
+struct ChainNodeFwdArgs {
+    const __bf16* x;            // [N][128]
+    const int32_t* seg_ptr;     // CSC segment offsets (col_ptr)
+    const __bf16* agg_z;        // edge MLP z [E][128]
+    const float* agg_rden;      // edge MLP rden [E]
+    const float* agg_scale;     // edge MLP RMSNorm scale [128]
+    const __bf16* wpack;        // node MLP forward 16x16x32 fragments (layer 0: K = 256)
+    int64_t woff[4];
+    int32_t wks[4];
+    const float* bias[4];
+    const float* scale;
+    float dinv;
+    int64_t M, ntiles;
+    __bf16* out;                // x_out = x + MLP
+    __bf16* aggr_save;          // [N][128]
+    __bf16* z_save;
+    float* rden_save;
+    __bf16* act8;
+    int64_t act_off[4];
+    unsigned* mask32;
+    int64_t mask_stride;        // 64-bit words per layer
+};
+
+struct ChainNodeBwdArgs {
+    const __bf16* dout;         // dx_out [N][128]
+    const __bf16* z_save;
+    const float* rden_save;
+    const float* scale;
+    float dinv;
+    const unsigned* mask32;
+    int64_t mask_stride;
+    const __bf16* wtpack;       // node MLP transposed 16x16x32 fragments
+    int64_t woff[4];
+    int32_t wks[4];
+    int64_t M, ntiles;
+    __bf16* dz8;
+    int64_t RP;
+    float* dscale_part;
+    __bf16* dx_part;            // dx_out + dA0[:, :128]
+    __bf16* d_aggr;             // dA0[:, 128:]
+};
+
 bool chain_eligible(const mgn_mlp* m);
+bool chain_node_eligible(const mgn_mlp* m);  // bf16, 256 -> 128 -> 128, 4 layers, RMSNorm
+int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
+                         const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
+                         hipStream_t st);
+int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
 int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
                        int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
 // nparts: number of dscale partial rows written (the reduction's row count)

@@ -29,7 +29,7 @@ constexpr int LFR = 32;                // fragments per layer: 8 out-tiles x 4 k
 constexpr int SLD = H + 8;             // scratch row stride (bf16)
 constexpr int SROWS = 8;               // scratch rows (one R8 octet per pass)
 constexpr size_t LDS_W = (size_t)4 * LFR * FRAG * 2;   // 128 KiB
-constexpr size_t LDS_V = (size_t)5 * H * 4;             // 4 bias vectors + scale / dscale reduction
+constexpr size_t LDS_V = (size_t)6 * H * 4;             // 4 bias vectors + scale (+ edge scale: node MLP)
 constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose scratch
 constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
 constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
@@ -472,14 +472,271 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------ node MLP
+// A-operand fragment (chain k order) read from a 16x16x32 pack in global memory (L2-resident):
+// source tile `tile` (relative to the layer base); two 8-byte pieces per lane.
+__device__ __forceinline__ bf16x8 gfrag(const __bf16* pack, int64_t tile, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+    const __bf16* p = pack + (tile * 64 + r) * 8 + 4 * (g & 1);
+    const u32x2 lo = *reinterpret_cast<const u32x2*>(p + 16 * (g >> 1) * 8);
+    const u32x2 hi = *reinterpret_cast<const u32x2*>(p + 16 * (2 + (g >> 1)) * 8);
+    const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, w);
+}
+
+// node layer 0 = x block (LDS image, layer slot 0) + aggr block (global fragments, tiles at
+// tile_of(t, s)); the aggr block's fragments of k-step s+1 load while k-step s computes
+template <class TileFn>
+__device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, const bf16x8 (&Bx)[4],
+                                              const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
+    gemm16(acc, W, 0, Bx, lane);
+    bf16x8 fr[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) fr[t] = gfrag(pack, tile_of(t, 0), lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        bf16x8 nf[8];
+        if (s + 1 < 4) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) nf[t] = gfrag(pack, tile_of(t, s + 1), lane);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], Ba[s], acc[t]);
+        if (s + 1 < 4) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) fr[t] = nf[t];
+        }
+    }
+}
+
+__global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // bias[4][H], scale[H], edge scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    const int m = lane & 15, g = lane >> 4;
+    stage16(W, a.wpack, a.woff, a.wks, false);
+    for (int i = threadIdx.x; i < 6 * H; i += NW * 64)
+        vec[i] = i < 4 * H ? a.bias[i / H][i % H] : i < 5 * H ? a.scale[i - 4 * H] : a.agg_scale[i - 5 * H];
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    for (int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x; tile < a.ntiles; tile += stride) {
+        const int64_t row = tile * TR + m;
+        const bool ok = row < a.M;
+        const int64_t v = clamp_row(row, a.M);
+        // x rows (layer-0 B operand of the x block, and the residual)
+        bf16x8 xb[4];
+        {
+            const __bf16* xp = a.x + v * H + 4 * g;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const u32x2 lo = *reinterpret_cast<const u32x2*>(xp + 32 * s);
+                const u32x2 hi = *reinterpret_cast<const u32x2*>(xp + 32 * s + 16);
+                const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+                xb[s] = __builtin_bit_cast(bf16x8, w);
+            }
+        }
+        // aggregation over the node's in-edges (target-sorted: one contiguous segment), in the
+        // accumulator layout: the lane sums its 32 features of every message s_e ⊙ z_k / q_k
+        f4 agg[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) agg[t] = f4{0.f, 0.f, 0.f, 0.f};
+        {
+            int k = a.seg_ptr[v];
+            const int ke = ok ? a.seg_ptr[v + 1] : k;
+            for (; k < ke; k += 2) {
+                const bool two = k + 1 < ke;
+                const int k1 = two ? k + 1 : k;
+                u32x2 z0[8], z1[8];
+                const __bf16* zp0 = a.agg_z + (int64_t)k * H + 4 * g;
+                const __bf16* zp1 = a.agg_z + (int64_t)k1 * H + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    z0[t] = *reinterpret_cast<const u32x2*>(zp0 + 16 * t);
+                    z1[t] = *reinterpret_cast<const u32x2*>(zp1 + 16 * t);
+                }
+                const float r0 = __builtin_amdgcn_rcpf(a.agg_rden[k]);
+                const float r1 = two ? __builtin_amdgcn_rcpf(a.agg_rden[k1]) : 0.f;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const f4 sc = *reinterpret_cast<const f4*>(vec + 5 * H + 16 * t + 4 * g);
+                    agg[t] += sc * (bf4(z0[t]) * r0);
+                    agg[t] += sc * (bf4(z1[t]) * r1);
+                }
+            }
+        }
+        store_rows(agg, scr, a.aggr_save, tile, a.M, lane);
+        bf16x8 Ba[4];
+        to_operand(agg, Ba);
+        f4 acc[8];
+        bf16x8 B[4];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            if (l == 0)
+                gemm16_layer0(acc, W, xb, Ba, a.wpack + a.woff[0],
+                              [](int t, int s) { return (int64_t)(t * 8 + 4 + s); }, lane);
+            else
+                gemm16(acc, W, l, B, lane);
+            unsigned bits = 0u;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f4 b = *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float val = fmaxf(acc[t][r] + b[r], 0.f);
+                    acc[t][r] = val;
+                    bits = push_bit(bits, val);
+                }
+            }
+            to_operand(acc, B);
+            a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
+            store_r8(acc, scr, a.act8 + a.act_off[l + 1], tile, lane);
+        }
+        gemm16(acc, W, 3, B, lane);
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float z = acc[t][r] + b[r];
+                acc[t][r] = z;
+                ss = fmaf(z, z, ss);
+            }
+        }
+        ss += __shfl_xor(ss, 16);
+        ss += __shfl_xor(ss, 32);
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        const float rq = __builtin_amdgcn_rcpf(q);
+        if (g == 0 && ok) a.rden_save[row] = q;
+        store_rows(acc, scr, a.z_save, tile, a.M, lane);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[t][r] = fmaf(sc[r], acc[t][r] * rq, (float)xb[t >> 1][4 * (t & 1) + r]);
+        }
+        store_rows(acc, scr, a.out, tile, a.M, lane);
+    }
+}
+
+__global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
+    const int m = lane & 15, g = lane >> 4;
+    stage16(W, a.wtpack, a.woff, a.wks, true);
+    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
+    for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    for (int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x; tile < a.ntiles; tile += stride) {
+        const int64_t row = tile * TR + m;
+        const bool ok = row < a.M;
+        const int64_t v = clamp_row(row, a.M);
+        u32x2 d[8], zr[8];
+        const __bf16* dp = a.dout + v * H + 4 * g;
+        const __bf16* zp = a.z_save + v * H + 4 * g;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
+            zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
+        }
+        const float qd = a.rden_save[v];
+        unsigned mk[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mk[l] = ok ? a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] : 0u;
+        // RMSNorm backward (layers.py:59-74)
+        f4 acc[8];
+        float dot = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 dy = bf4(d[t]);
+            const f4 z = bf4(zr[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            acc[t] = dy;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dot = fmaf(sc[r] * dy[r], z[r], dot);
+        }
+        dot += __shfl_xor(dot, 16);
+        dot += __shfl_xor(dot, 32);
+        const float rq = __builtin_amdgcn_rcpf(qd);
+        const float rms = qd - RMS_EPS;
+        const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 z = bf4(zr[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            f4 ds;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dy = acc[t][r];
+                acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
+                ds[r] = row16_sum(ok ? dy * z[r] * rq : 0.f);
+            }
+            if (m == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * t + 4 * g) += ds;
+        }
+        bf16x8 B[4];
+        to_operand(acc, B);
+        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
+#pragma unroll
+        for (int l = 3; l >= 1; --l) {
+            gemm16(acc, W, l, B, lane);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[t][r] = __int_as_float(__float_as_int(acc[t][r]) & bit_sel(mk[l - 1], 4 * t + r));
+            to_operand(acc, B);
+            store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
+        }
+        // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
+        gemm16(acc, W, 0, B, lane);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
+        store_rows(acc, scr, a.dx_part, tile, a.M, lane);
+        {
+            const __bf16* pk = a.wtpack + a.woff[0];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                bf16x8 fr[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) fr[t] = gfrag(pk, (int64_t)((8 + t) * 4 + s), lane);
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], B[s], acc[t]);
+            }
+        }
+        store_rows(acc, scr, a.d_aggr, tile, a.M, lane);
+    }
+    __syncthreads();
+    if (threadIdx.x < H) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s2 += red[w * H + threadIdx.x];
+        a.dscale_part[(int64_t)blockIdx.x * H + threadIdx.x] = s2;
+    }
+}
+
 int set_lds_once(const void* fn, size_t bytes) {
     static std::mutex mu;
-    static bool done[2] = {false, false};
+    static const void* done[8] = {};
     std::lock_guard<std::mutex> lk(mu);
-    const int slot = fn == (const void*)chain16_fwd_kernel ? 0 : 1;
-    if (done[slot]) return 0;
+    for (const void* d : done)
+        if (d == fn) return 0;
     MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-    done[slot] = true;
+    for (const void*& d : done)
+        if (!d) {
+            d = fn;
+            break;
+        }
     return 0;
 }
 
@@ -545,6 +802,81 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = grid;
     ProfScope ps(PROF_BWD_EDGE, st);
     hipLaunchKernelGGL(chain16_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+// node tiles are few (N/16): one workgroup per CU, tiles spread wave-major over all of them
+static int node_grid(int64_t ntiles) {
+    int cus = chain16_grid((int64_t)1 << 30);
+    return (int)(ntiles < cus ? ntiles : cus);
+}
+
+bool chain_node_eligible(const mgn_mlp* m) {
+    return m->dtype == MGN_BF16 && m->hidden == H && m->in_dim == 2 * H && m->out_dim == H && m->n_layers == 4 &&
+           m->has_norm;
+}
+
+int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
+                         const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
+                         hipStream_t st) {
+    ChainNodeFwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = reinterpret_cast<const __bf16*>(x);
+    a.seg_ptr = t->col_ptr;
+    a.agg_z = reinterpret_cast<const __bf16*>(edge_sv->z);
+    a.agg_rden = edge_sv->rden;
+    a.agg_scale = edge->scale;
+    a.wpack = reinterpret_cast<const __bf16*>(m->wpack);
+    layer_offsets(m, a.woff, a.wks);
+    for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;
+    a.out = reinterpret_cast<__bf16*>(x_out);
+    a.aggr_save = reinterpret_cast<__bf16*>(aggr_save);
+    a.z_save = reinterpret_cast<__bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.act8 = reinterpret_cast<__bf16*>(sv->act);
+    for (int l = 0; l < 4; ++l) a.act_off[l] = act_off(*m, M, l, 1);
+    a.mask32 = reinterpret_cast<unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    if (M == 0) return 0;
+    if (int e2 = set_lds_once((const void*)chain16_node_fwd_kernel, LDS_TOTAL)) return e2;
+    ProfScope ps(PROF_FWD_NODE, st);
+    hipLaunchKernelGGL(chain16_node_fwd_kernel, dim3(node_grid(a.ntiles)), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st) {
+    ChainNodeBwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dout = reinterpret_cast<const __bf16*>(dout);
+    a.z_save = reinterpret_cast<const __bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
+    layer_offsets(m, a.woff, a.wks);
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;
+    a.dz8 = reinterpret_cast<__bf16*>(dz8);
+    a.RP = rows_pad(M);
+    a.dscale_part = dscale_part;
+    a.dx_part = reinterpret_cast<__bf16*>(dx_part);
+    a.d_aggr = reinterpret_cast<__bf16*>(d_aggr);
+    *nparts = 0;
+    if (M == 0) return 0;
+    if (int e2 = set_lds_once((const void*)chain16_node_bwd_kernel, LDS_TOTAL)) return e2;
+    const int grid = node_grid(a.ntiles);
+    *nparts = grid;
+    ProfScope ps(PROF_BWD_NODE, st);
+    hipLaunchKernelGGL(chain16_node_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

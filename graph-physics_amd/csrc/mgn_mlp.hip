@@ -1340,7 +1340,9 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
-    const int64_t ntiles = rows_pad(M) / 32;  // dscale partial rows: the smallest tile over modes
+    // dscale partial rows: the most any backward kernel writes (generic: one per 32-row tile;
+    // chained node kernel: one per workgroup, at most one per 16-row tile)
+    const int64_t ntiles = rows_pad(M) / 16;
     const int64_t nchunks = wgrad_max_chunks(rows_pad(M));
     size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
@@ -1747,6 +1749,8 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
                                    nullptr, nullptr, st)) {
         return r;
     }
+    if (chain && chain_variant() == 16 && chain_node_eligible(node))
+        return chain16_node_forward(node, x, t, edge, &saved->edge, t->num_nodes, x_out, saved->aggr, &saved->node, st);
     MlpIn nin;
     memset(&nin, 0, sizeof(nin));
     nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
@@ -1814,9 +1818,26 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     on.mode = MODE_NODE;
     on.o1 = dx_part;
     on.o2 = d_aggr;
-    if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on, node_grads,
-                                  mlp_ws, mlp_ws_bytes, st))
+    if (chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) && t->num_nodes > 0) {
+        // chained data gradients, then the node MLP's weight gradients on the same workspace carve
+        const int64_t Nn = t->num_nodes;
+        MGN_REQUIRE(mlp_ws_bytes >= mlp_bwd_ws(node, Nn), "backward workspace too small");
+        char* q = reinterpret_cast<char*>(mlp_ws);
+        void* ndz = q;
+        q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * 2);
+        float* ndsp = reinterpret_cast<float*>(q);
+        q += align_up((size_t)(rows_pad(Nn) / 16) * node->out_dim * sizeof(float));  // = mlp_bwd_ws carve
+        float* npart = reinterpret_cast<float*>(q);
+        int nparts = 0;
+        if (int r = chain16_node_backward(node, Nn, &saved->node, dx_out, ndz, ndsp, &nparts, dx_part, d_aggr, st))
+            return r;
+        if (int r = mlp_wgrad_any(node, Nn, saved->node.act, ndz, ndsp, nparts, npart, node_grads, &nin, 0, nullptr,
+                                  true, st))
+            return r;
+    } else if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on,
+                                         node_grads, mlp_ws, mlp_ws_bytes, st)) {
         return r;
+    }
     // edge MLP data gradients: dY = de_out + d_aggr[dst] -> de = de_out + dZ0·W0a, dZ0 (row-major)
     const int64_t E = t->num_edges, N = t->num_nodes;
     MGN_REQUIRE(mlp_ws_bytes >= mlp_bwd_ws(edge, E), "backward workspace too small");
