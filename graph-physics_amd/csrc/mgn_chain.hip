@@ -575,14 +575,7 @@ int ablate_env() {
 }
 
 int chain_grid(int64_t ntiles) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            cus = n;
-        else
-            cus = 256;
-    }
+    const int cus = device_cus();
     const int64_t groups = cdiv64(ntiles, NW);
     return (int)(groups < cus ? groups : cus);
 }

@@ -180,15 +180,7 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
 }
 
 int chain16_grid(int64_t ntiles) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            cus = n;
-        else
-            cus = 256;
-    }
+    const int cus = device_cus();
     const int64_t groups = cdiv64(ntiles, NW);
     return (int)(groups < cus ? groups : cus);
 }

@@ -173,6 +173,19 @@ __host__ __device__ __forceinline__ int64_t r8_index(int64_t m, int64_t c, int64
     return ((m >> 3) * cols + c) * 8 + (m & 7);
 }
 // Saved buffers cover rows padded to 64 (every tile, including pure-padding rows, is written).
+// compute units of the current device (read once; 256 on MI355X)
+inline int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
 __host__ __device__ __forceinline__ int64_t rows_pad(int64_t M) { return (M + 63) / 64 * 64; }
 __host__ __device__ __forceinline__ int kstep_of(int dtype) { return dtype == MGN_BF16 ? 32 : 4; }
 // R8 column count of the saved INPUT of layer l (layer 0: padded MLP input; else padded hidden)

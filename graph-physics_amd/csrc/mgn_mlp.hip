@@ -764,14 +764,11 @@ struct WgArgs {
 constexpr int WG_GROUPS = 2;
 
 template <class T, int H>
-constexpr int wg_tile_floats() {
-    return TileCfg<H / 16, H / 16>::NTW * TileCfg<H / 16, H / 16>::MTW * 4 + TileCfg<H / 16, H / 16>::NTW;
-}
-
-template <class T, int H>
 size_t wgrad_lds_bytes(bool staged) {
-    const size_t stage = staged ? (size_t)WG_GROUPS * 2 * H * (64 + 16 / sizeof(T)) * sizeof(T) : 0;
-    const size_t red = (size_t)MGN_THREADS * wg_tile_floats<T, H>() * sizeof(float);
+    // re-gathered layer-0 input: [2][H][64 + pad] per group; bf16 R8 input: [2][8 octets][H] x 16 B
+    const size_t stage = staged ? (size_t)WG_GROUPS * 2 * H * (64 + 16 / sizeof(T)) * sizeof(T)
+                                : (sizeof(T) == 2 ? (size_t)WG_GROUPS * 2 * 8 * H * 16 : 0);
+    const size_t red = (size_t)(H * (H + 4) + H) * sizeof(float);  // canonical combine tile + bias row
     return stage > red ? stage : red;
 }
 
@@ -821,7 +818,85 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             }
         }
     };
-    if (!staged) {
+    // Stage pipeline shared by the LDS-staged paths: the groups take alternate SR-row stages; the
+    // next stage's X source loads AND its dZ fragments are issued before this stage's MFMAs, so a
+    // stage exposes at most one memory latency (with two waves per SIMD the dZ loads issued inside
+    // the k-loop used to expose one per k-step). Double-buffered LDS, one barrier per stage; every
+    // group runs the same iteration count (a group past the end stages zeros) so all threads reach
+    // each barrier. Loads past r_end are clamped to a valid stage and never consumed.
+    constexpr int KS = SR / KSTEP;
+    auto pipeline = [&](auto&& issue_x, auto&& commit_x, auto&& frag_b) {
+        typename Mf<T>::frag zn[KS][C::NTW];
+        auto issue_z = [&](int64_t m0) {
+            const int64_t mc = m0 < r_end ? m0 : r_begin;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+                    zn[ks][i] = ld_frag(Z + r8_index(mc + ks * KSTEP + VEC * (lane >> 4), (nt0 + i) * 16 + (lane & 15), H));
+        };
+        issue_x(r_begin + grp * SR);
+        issue_z(r_begin + grp * SR);
+        for (int64_t base = r_begin; base < r_end; base += WG_GROUPS * SR) {
+            const int64_t m0 = base + grp * SR;
+            const int par = (int)((base - r_begin) / (WG_GROUPS * SR) & 1);
+            commit_x(par);
+            typename Mf<T>::frag za[KS][C::NTW];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i) za[ks][i] = zn[ks][i];
+            __syncthreads();
+            issue_x(m0 + WG_GROUPS * SR);
+            issue_z(m0 + WG_GROUPS * SR);
+            if (active && m0 < r_end) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    typename Mf<T>::frag fb[C::MTW];
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) fb[j] = kon[j] ? frag_b(par, ks, j) : zero;
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                        for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(za[ks][i], fb[j], acc[i][j]);
+                    if (do_bias) bias_acc(za[ks]);
+                }
+            }
+        }
+    };
+    if (!staged && VEC == 8) {
+        // R8 input: the 4 waves of a group all need the same 8 X fragments per k-step, so the
+        // group copies each stage once (SR/8 octets x H columns x 16 B, coalesced: in R8 an
+        // octet's columns are contiguous) and the waves read their fragments from LDS (lanes 0-15
+        // = 16 consecutive columns: conflict-free).
+        constexpr int ITEMS = (SR / 8) * H;
+        constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;
+        u32x4* img = reinterpret_cast<u32x4*>(smem) + (size_t)grp * 2 * ITEMS;
+        u32x4 nxt[PER];
+        pipeline(
+            [&](int64_t m0) {
+                const int64_t mc = m0 < r_end ? m0 : r_begin;
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    const int it = tid + q * MGN_THREADS;
+                    const int o = it / H, c = it % H;
+                    const int cc = col0 + c < job.kp ? col0 + c : 0;
+                    nxt[q] = *reinterpret_cast<const u32x4*>(X + r8_index(mc + 8 * (it < ITEMS ? o : 0), cc, job.kp));
+                    if (col0 + c >= job.kp) nxt[q] = u32x4{0u, 0u, 0u, 0u};
+                }
+            },
+            [&](int par) {
+                u32x4* buf = img + (size_t)par * ITEMS;
+#pragma unroll
+                for (int q = 0; q < PER; ++q)
+                    if (tid + q * MGN_THREADS < ITEMS) buf[tid + q * MGN_THREADS] = nxt[q];
+            },
+            [&](int par, int ks, int j) {
+                const u32x4* buf = img + (size_t)par * ITEMS;
+                return ld_frag(reinterpret_cast<const T*>(buf + (ks * (KSTEP / 8) + (lane >> 4)) * H + (mt0 + j) * 16 +
+                                                          (lane & 15)));
+            });
+    } else if (!staged) {
 #pragma unroll 2
         for (int64_t m0 = r_begin + grp * KSTEP; m0 < r_end; m0 += WG_GROUPS * KSTEP) {
             if (!active) break;
@@ -839,114 +914,101 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             if (do_bias) bias_acc(fa);
         }
     } else {
-        // segment holding columns [col0, col0 + H) of the layer-0 input (segments are H wide)
+        // re-gathered layer-0 input: segment holding columns [col0, col0 + H) (segments are H
+        // wide); consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the
+        // transposed LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots.
         int s = 0;
         while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
         const SrcSeg g = a.seg[s];
         const T* src = reinterpret_cast<const T*>(g.p);
-        // consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the transposed
-        // LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots: conflict-free.
-        // Double buffered: the next stage's loads are in flight while this stage's MFMAs run.
-        // The groups take alternate SR-row stages; both run the same number of iterations (a group
-        // past the end stages zeros) so every workgroup barrier is reached by all threads.
         constexpr int ITEMS = SR * (H / CH);
         constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;  // 16-byte chunks per thread
-
         u32x4 nxt[PER];
-        auto issue = [&](int64_t m0) {
+        pipeline(
+            [&](int64_t m0) {
 #pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int it = tid + q * MGN_THREADS;
-                const int r = it % SR, cc = (it / SR) * CH;
-                const int64_t row = m0 + r;
-                nxt[q] = u32x4{0u, 0u, 0u, 0u};
-                if (it < ITEMS && m0 < r_end && row < a.M) {
-                    const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
-                    nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + (col0 - g.coff) + cc);
+                for (int q = 0; q < PER; ++q) {
+                    const int it = tid + q * MGN_THREADS;
+                    const int r = it % SR, cc = (it / SR) * CH;
+                    const int64_t row = m0 + r;
+                    nxt[q] = u32x4{0u, 0u, 0u, 0u};
+                    if (it < ITEMS && m0 < r_end && row < a.M) {
+                        const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
+                        nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + (col0 - g.coff) + cc);
+                    }
                 }
-            }
-        };
-        issue(r_begin + grp * SR);
-        for (int64_t base = r_begin; base < r_end; base += WG_GROUPS * SR) {
-            const int64_t m0 = base + grp * SR;
-            T* buf = AT + (size_t)((base - r_begin) / (WG_GROUPS * SR) & 1) * H * LDT;
+            },
+            [&](int par) {
+                T* buf = AT + (size_t)par * H * LDT;
 #pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int it = tid + q * MGN_THREADS;
-                if (it >= ITEMS) continue;
-                const int r = it % SR, cc = (it / SR) * CH;
-                const T* v = reinterpret_cast<const T*>(&nxt[q]);
+                for (int q = 0; q < PER; ++q) {
+                    const int it = tid + q * MGN_THREADS;
+                    if (it >= ITEMS) continue;
+                    const int r = it % SR, cc = (it / SR) * CH;
+                    const T* v = reinterpret_cast<const T*>(&nxt[q]);
 #pragma unroll
-                for (int e = 0; e < CH; ++e) buf[(size_t)(cc + e) * LDT + r] = v[e];
-            }
-            __syncthreads();
-            issue(m0 + WG_GROUPS * SR);
-            if (active && m0 < r_end) {
-#pragma unroll
-                for (int ks = 0; ks < SR / KSTEP; ++ks) {
-                    const int64_t mr = m0 + ks * KSTEP + VEC * (lane >> 4);
-                    typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
-#pragma unroll
-                    for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
-#pragma unroll
-                    for (int j = 0; j < C::MTW; ++j)
-                        fb[j] = ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
-#pragma unroll
-                    for (int i = 0; i < C::NTW; ++i)
-#pragma unroll
-                        for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
-                    if (do_bias) bias_acc(fa);
+                    for (int e = 0; e < CH; ++e) buf[(size_t)(cc + e) * LDT + r] = v[e];
                 }
-            }
-        }
+            },
+            [&](int par, int ks, int j) {
+                const T* buf = AT + (size_t)par * H * LDT;
+                return ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+            });
     }
-    // group 1 hands its tile to group 0 through LDS (layout [value][thread]: conflict-free)
-    constexpr int TF = wg_tile_floats<T, H>();
-    float* red = reinterpret_cast<float*>(smem);
-    __syncthreads();  // staging buffers are dead
-    if (grp == 1) {
+    // Combine and store through a canonical [n][k] tile in LDS (row pitch H+4 floats: the four
+    // 16-lane groups of an accumulator write land 16 banks apart): group 1 deposits its tile,
+    // group 0 adds its own, then all 512 threads store the slab rows with coalesced 16-byte stores
+    // (the per-lane accumulator layout holds 4 rows x 1 column: scalar stores 4 rows apart).
+    constexpr int LP = H + 4;
+    float* tile = reinterpret_cast<float*>(smem);
+    float* btile = tile + H * LP;
+    float bt[C::NTW];
+#pragma unroll
+    for (int i = 0; i < C::NTW; ++i) {
+        float t = bsum[i];
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        bt[i] = t;
+    }
+    auto deposit = [&](bool add) {
 #pragma unroll
         for (int i = 0; i < C::NTW; ++i) {
 #pragma unroll
             for (int j = 0; j < C::MTW; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) red[((i * C::MTW + j) * 4 + r) * MGN_THREADS + tid] = acc[i][j][r];
-            red[(C::NTW * C::MTW * 4 + i) * MGN_THREADS + tid] = bsum[i];
-        }
-    }
-    __syncthreads();
-    if (grp == 1 || !active) return;
-#pragma unroll
-    for (int i = 0; i < C::NTW; ++i) {
-#pragma unroll
-        for (int j = 0; j < C::MTW; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((i * C::MTW + j) * 4 + r) * MGN_THREADS + tid];
-        bsum[i] += red[(C::NTW * C::MTW * 4 + i) * MGN_THREADS + tid];
-    }
-    static_assert(TF == C::NTW * C::MTW * 4 + C::NTW, "tile layout");
-    float* part = a.part + (int64_t)blockIdx.x * a.G;
-#pragma unroll
-    for (int i = 0; i < C::NTW; ++i)
-#pragma unroll
-        for (int j = 0; j < C::MTW; ++j) {
-            const int kc = col0 + (mt0 + j) * 16 + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = (nt0 + i) * 16 + (lane >> 4) * 4 + r;
-                if (n < job.n && kc < job.k) part[job.w_off + (int64_t)n * job.k + kc] = acc[i][j][r];
+                for (int r = 0; r < 4; ++r) {
+                    float* p = tile + ((nt0 + i) * 16 + (lane >> 4) * 4 + r) * LP + (mt0 + j) * 16 + (lane & 15);
+                    *p = add ? *p + acc[i][j][r] : acc[i][j][r];
+                }
+            if (do_bias && lane < 16) {
+                float* p = btile + (nt0 + i) * 16 + lane;
+                *p = add ? *p + bt[i] : bt[i];
             }
         }
-    if (do_bias) {
+    };
+    __syncthreads();  // staging buffers are dead
+    if (grp == 1 && active) deposit(false);
+    __syncthreads();
+    if (grp == 0 && active) deposit(true);
+    __syncthreads();
+    float* part = a.part + (int64_t)blockIdx.x * a.G;
+    constexpr int C4 = H / 4;
+    const bool vec = ((a.G | job.w_off | (int64_t)job.k) & 3) == 0;
+    for (int it = threadIdx.x; it < H * C4; it += MGN_THREADS * WG_GROUPS) {
+        const int n = it / C4, k4 = (it % C4) * 4;
+        const int kc = col0 + k4;
+        if (n >= job.n || kc >= job.k) continue;
+        const f4 v = *reinterpret_cast<const f4*>(tile + n * LP + k4);
+        float* dst = part + job.w_off + (int64_t)n * job.k + kc;
+        if (vec && kc + 4 <= job.k) {
+            *reinterpret_cast<f4*>(dst) = v;
+        } else {
 #pragma unroll
-        for (int i = 0; i < C::NTW; ++i) {
-            float t = bsum[i];
-            t += __shfl_xor(t, 16);
-            t += __shfl_xor(t, 32);
-            const int n = (nt0 + i) * 16 + lane;
-            if (lane < 16 && n < job.n) part[job.b_off + n] = t;
+            for (int e = 0; e < 4; ++e)
+                if (kc + e < job.k) dst[e] = v[e];
         }
     }
+    if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
 }
 
 // grads[g] = Σ_c part[c][g] for g < G (blocks [0, ceil(G/64)): 64 outputs x 4 chunk groups each);
@@ -1209,9 +1271,12 @@ int64_t grad_G(const mgn_mlp* m) {
 }
 
 // rows per chunk: enough workgroups to fill the chip (~512), at most 64 partial slabs
+// one 512-thread workgroup per CU fits (VGPRs + LDS), so chunks x jobs stays within one wave of
+// workgroups over the CUs (a second, partial round doubles a short launch)
 int wgrad_rows_per_chunk(int64_t RP, int njobs) {
-    int64_t chunks = cdiv64(512, njobs);
+    int64_t chunks = device_cus() / njobs;
     if (chunks > 64) chunks = 64;
+    if (chunks < 1) chunks = 1;
     int64_t r = cdiv64(RP, chunks);
     r = cdiv64(r, 64) * 64;
     if (r < 64) r = 64;
