@@ -913,6 +913,60 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
             if (do_bias) bias_acc(fa);
         }
+    } else if (VEC == 8 && H == 128) {
+        if constexpr (VEC == 8 && H == 128) {
+            // re-gathered layer-0 input, bf16 h=128: rows staged ROW-major (consecutive threads take
+            // consecutive 16-byte chunks of one row: coalesced 256-byte row reads, one ds_write_b128
+            // each) and the column-major B fragments read back with ds_read_b64_tr_b16 (two 4-row
+            // blocks per fragment). Chunk ch of row r sits at slot ch ^ swz(r), which keeps both the
+            // row writes and the transposed reads (a 32-lane half = two blocks 8 rows apart, same
+            // columns) conflict-free.
+            int s = 0;
+            while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
+            const SrcSeg g = a.seg[s];
+            const T* src = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
+            constexpr int CPR = H / 8;                        // 16-byte chunks per row
+            constexpr int ITEMS = SR * CPR;
+            constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;
+            char* img = smem + (size_t)grp * 2 * SR * H * sizeof(T);
+            auto slot = [](int r, int ch) { return r * (H * (int)sizeof(T)) + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); };
+            u32x4 nxt[PER];
+            pipeline(
+                [&](int64_t m0) {
+    #pragma unroll
+                    for (int q = 0; q < PER; ++q) {
+                        const int it = tid + q * MGN_THREADS;
+                        const int r = (it / CPR) % SR, ch = it % CPR;
+                        const int64_t row = m0 + r;
+                        const bool ok = it < ITEMS && m0 < r_end && row < a.M;
+                        const int64_t rc = ok ? row : 0;
+                        const int64_t sr = g.idx ? (int64_t)g.idx[rc] : rc;
+                        nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + ch * 8);
+                        if (!ok) nxt[q] = u32x4{0u, 0u, 0u, 0u};
+                    }
+                },
+                [&](int par) {
+                    char* buf = img + (size_t)par * SR * H * sizeof(T);
+    #pragma unroll
+                    for (int q = 0; q < PER; ++q) {
+                        const int it = tid + q * MGN_THREADS;
+                        if (it < ITEMS) *reinterpret_cast<u32x4*>(buf + slot(it / CPR, it % CPR)) = nxt[q];
+                    }
+                },
+                [&](int par, int ks, int j) {
+                    typedef short s4 __attribute__((ext_vector_type(4)));
+                    typedef __attribute__((address_space(3))) s4 lds_s4;
+                    const char* buf = img + (size_t)par * SR * H * sizeof(T);
+                    const int i = lane & 15, q = i >> 2, p = i & 3;
+                    const int r0 = ks * KSTEP + 8 * (lane >> 4) + q;
+                    const int ch = (mt0 + j) * 2 + (p >> 1);
+                    const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(buf + slot(r0, ch) + 8 * (p & 1)));
+                    const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(buf + slot(r0 + 4, ch) + 8 * (p & 1)));
+                    typedef short s8 __attribute__((ext_vector_type(8)));
+                    const s8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    return __builtin_bit_cast(typename Mf<T>::frag, v);
+                });
+        }
     } else {
         // re-gathered layer-0 input: segment holding columns [col0, col0 + H) (segments are H
         // wide); consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the
