@@ -776,7 +776,7 @@ template <class T, int H>
 __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
     constexpr int NT = H / 16;
-    constexpr int SR = 64;                      // rows per LDS stage (re-gathered layer-0 input)
+    constexpr int SR = 64;                      // rows per LDS stage
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int LDT = SR + CH;                // LDS row = one input column over SR rows (+pad)
     using C = TileCfg<NT, NT>;
@@ -1065,21 +1065,198 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
 }
 
+// Ring variant for bf16 h=128 (the hot configuration): the whole workgroup (8 waves as 4 n-groups
+// x 2 k-groups, 2x4 16x16 tiles each) consumes one 32-row stage at a time from an 8-slot LDS ring
+// filled by global_load_lds (LDS-DMA: no VGPR staging, so 7 stages = 112 KiB stay in flight per
+// CU). A stage is the dZ block (R8: 8 KiB contiguous) and the X block (R8 octets, or re-gathered
+// rows in the XOR-swizzled row image read by ds_read_b64_tr_b16; the swizzle is applied on the
+// source addresses since LDS-DMA writes lane-linear). Each wave issues one 1 KiB piece of each per
+// stage; a counted vmcnt + barrier publishes stage s while stages s+1..s+6 stay in flight. No group
+// combine: every wave deposits its own tiles into the canonical LDS tile for the slab stores.
+constexpr int RG_RS = 32;                 // rows per stage (one MFMA k-step)
+constexpr int RG_NS = 8;                  // ring slots
+constexpr int RG_SLOT = 2 * RG_RS * 128 * 2;  // dZ + X, bf16 h=128: 16 KiB
+constexpr size_t RG_LDS = (size_t)RG_NS * RG_SLOT;
+
+// A ring job is self-contained (its own dZ block, X source, row space, chunking and slab target),
+// so one launch can cover several MLPs: WG b runs job j with wg0_j <= b < wg0_j + nchunks_j.
+struct RgJob {
+    const void* z;      // dZ: R8 [RP][128] block of this layer
+    const void* x;      // X: R8 matrix (ld == 0, kp columns) or row-major rows (ld = row stride), both
+                        // already offset to this job's first column
+    int64_t ld, RP, M;
+    float* part;        // slab base of the job's MLP; slab c at part + c * G
+    int64_t G, w_off, b_off;
+    int32_t n, k, kp, col0;
+    int32_t rows_per_chunk, nchunks, wg0, pad;
+};
+struct RgArgs {
+    int32_t njobs, pad;
+    RgJob job[12];
+};
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int rg_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+__global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
+    constexpr int H = 128;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wn = w & 3, wk = w >> 2;
+    int jn = 0;
+    while (jn + 1 < a.njobs && (int)blockIdx.x >= a.job[jn + 1].wg0) ++jn;
+    const RgJob job = a.job[jn];
+    const int chunk = (int)blockIdx.x - job.wg0;
+    const int64_t r_begin = (int64_t)chunk * job.rows_per_chunk;
+    const int64_t r_end = r_begin + job.rows_per_chunk < job.RP ? r_begin + job.rows_per_chunk : job.RP;
+    const int nst = r_end > r_begin ? (int)((r_end - r_begin) / RG_RS) : 0;  // 0: zero slab
+    const int col0 = job.col0;
+    const bool staged = job.ld != 0;
+    const __bf16* Z = reinterpret_cast<const __bf16*>(job.z);
+    const __bf16* X = reinterpret_cast<const __bf16*>(job.x);
+    // this lane's piece of a gathered stage: row 4w + (lane>>4), source chunk for its LDS slot
+    const int gr = 4 * w + (lane >> 4), gch = (lane & 15) ^ rg_swz(gr);
+    auto issue = [&](int s) {
+        const int sc = s < nst ? s : nst - 1;  // past the end: reload the last stage, never consumed
+        const int64_t m0 = r_begin + (int64_t)sc * RG_RS;
+        char* slot = smem + (s % RG_NS) * RG_SLOT;
+        glds16(Z + m0 * H + w * 512 + lane * 8, slot + w * 1024);
+        const __bf16* xs;
+        if (!staged) {
+            xs = X + (((m0 >> 3) + (w >> 1)) * job.kp + (w & 1) * 64 + lane) * 8;
+        } else {
+            const int64_t row = m0 + gr < job.M ? m0 + gr : job.M - 1;
+            xs = X + row * job.ld + gch * 8;
+        }
+        glds16(xs, slot + RG_SLOT / 2 + w * 1024);
+    };
+    f4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float bsum[2] = {0.f, 0.f};
+    const bool do_bias = job.b_off >= 0 && wk == 0;
+    if (nst > 0) {
+#pragma unroll
+        for (int p = 0; p < RG_NS - 1; ++p) issue(p);
+    }
+    for (int s = 0; s < nst; ++s) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (RG_NS - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(s + RG_NS - 1);
+        const char* zi = smem + (s % RG_NS) * RG_SLOT;
+        const char* xi = zi + RG_SLOT / 2;
+        bf16x8 fa[2], fb[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            fa[i] = *reinterpret_cast<const bf16x8*>(zi + ((lane >> 4) * H + (2 * wn + i) * 16 + (lane & 15)) * 16);
+        if (!staged) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                fb[j] = *reinterpret_cast<const bf16x8*>(xi + ((lane >> 4) * H + (4 * wk + j) * 16 + (lane & 15)) * 16);
+        } else {
+            // inline asm: with the builtin, hipcc waits vmcnt(0) (drains the ring) before the
+            // transposed reads, assuming they may alias the in-flight LDS-DMA; the trailing wait
+            // carries the values so no consumer is scheduled above it
+            const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+            const int r0 = 8 * (lane >> 4) + q;
+            const unsigned base = (unsigned)(uintptr_t)(xi);
+            u32x2 lo[4], hi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = (4 * wk + j) * 2 + (p >> 1);
+                const unsigned a0 = base + r0 * (H * 2) + 16 * (ch ^ rg_swz(r0)) + 8 * (p & 1);
+                const unsigned a1 = base + (r0 + 4) * (H * 2) + 16 * (ch ^ rg_swz(r0 + 4)) + 8 * (p & 1);
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[j]) : "v"(a0));
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi[j]) : "v"(a1));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]),
+                           "+v"(hi[3]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 v = {lo[j][0], lo[j][1], hi[j][0], hi[j][1]};
+                fb[j] = __builtin_bit_cast(bf16x8, v);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        if (do_bias) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int v = 0; v < 8; ++v) bsum[i] += (float)fa[i][v];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (unconsumed) ring loads
+    __syncthreads();
+    // canonical tile (row pitch H+4 floats) + bias row, then coalesced slab stores (as mlp_wgrad_kernel)
+    constexpr int LP = H + 4;
+    float* tile = reinterpret_cast<float*>(smem);
+    float* btile = tile + H * LP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                tile[((2 * wn + i) * 16 + (lane >> 4) * 4 + r) * LP + (4 * wk + j) * 16 + (lane & 15)] = acc[i][j][r];
+        float t = bsum[i];
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        if (do_bias && lane < 16) btile[(2 * wn + i) * 16 + lane] = t;
+    }
+    __syncthreads();
+    float* part = job.part + (int64_t)chunk * job.G;
+    constexpr int C4 = H / 4;
+    const bool vec = ((job.G | job.w_off | (int64_t)job.k) & 3) == 0;
+    for (int it = threadIdx.x; it < H * C4; it += 512) {
+        const int n = it / C4, k4 = (it % C4) * 4;
+        const int kc = col0 + k4;
+        if (n >= job.n || kc >= job.k) continue;
+        const f4 v = *reinterpret_cast<const f4*>(tile + n * LP + k4);
+        float* dst = part + job.w_off + (int64_t)n * job.k + kc;
+        if (vec && kc + 4 <= job.k) {
+            *reinterpret_cast<f4*>(dst) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (kc + e < job.k) dst[e] = v[e];
+        }
+    }
+    if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
+}
+
 // grads[g] = Σ_c part[c][g] for g < G (blocks [0, ceil(G/64)): 64 outputs x 4 chunk groups each);
 // grads[G + s] = Σ_t dscale_part[t][s] (one block per s). Fixed summation order: deterministic.
-__global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(const float* __restrict__ part, int nchunks,
-                                                                   int64_t G, const float* __restrict__ dsp,
-                                                                   int ntiles, int NS, float* __restrict__ grads) {
-    __shared__ float red[MGN_THREADS];
-    const int64_t gblocks = (G + 63) / 64;
+struct RedDesc {
+    const float* part;
+    const float* dsp;
+    float* grads;
+    int64_t G;
+    int32_t nchunks, ntiles, NS, blocks;
+};
+
+__device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float* red) {
+    const int64_t gblocks = (d.G + 63) / 64;
     const int tid = threadIdx.x;
-    if ((int64_t)blockIdx.x < gblocks) {
-        const int64_t g = (int64_t)blockIdx.x * 64 + (tid & 63);
+    const float* part = d.part;
+    const int64_t G = d.G;
+    if (b < gblocks) {
+        const int64_t g = b * 64 + (tid & 63);
         const int cg = tid >> 6;
         float s = 0.f;
         if (g < G) {
             int c = cg;
-            for (; c + 12 < nchunks; c += 16) {
+            for (; c + 12 < d.nchunks; c += 16) {
                 const float v0 = part[(int64_t)c * G + g], v1 = part[(int64_t)(c + 4) * G + g];
                 const float v2 = part[(int64_t)(c + 8) * G + g], v3 = part[(int64_t)(c + 12) * G + g];
                 s += v0;
@@ -1087,23 +1264,37 @@ __global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(const float* 
                 s += v2;
                 s += v3;
             }
-            for (; c < nchunks; c += 4) s += part[(int64_t)c * G + g];
+            for (; c < d.nchunks; c += 4) s += part[(int64_t)c * G + g];
         }
         red[tid] = s;
         __syncthreads();
-        if (tid < 64 && g < G) grads[g] = ((red[tid] + red[tid + 64]) + red[tid + 128]) + red[tid + 192];
+        if (tid < 64 && g < G) d.grads[g] = ((red[tid] + red[tid + 64]) + red[tid + 128]) + red[tid + 192];
     } else {
-        const int sidx = (int)(blockIdx.x - gblocks);
+        const int sidx = (int)(b - gblocks);
         float s = 0.f;
-        for (int t = tid; t < ntiles; t += MGN_THREADS) s += dsp[(int64_t)t * NS + sidx];
+        for (int t = tid; t < d.ntiles; t += MGN_THREADS) s += d.dsp[(int64_t)t * d.NS + sidx];
         red[tid] = s;
         __syncthreads();
         for (int w = MGN_THREADS / 2; w > 0; w >>= 1) {
             if (tid < w) red[tid] += red[tid + w];
             __syncthreads();
         }
-        if (tid == 0) grads[G + sidx] = red[0];
+        if (tid == 0) d.grads[G + sidx] = red[0];
     }
+}
+
+// one launch reducing up to two MLPs (blocks of desc 0, then desc 1)
+struct RedArgs {
+    RedDesc d[2];
+    int32_t nd, pad;
+};
+__global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(RedArgs a) {
+    __shared__ float red[MGN_THREADS];
+    const int64_t b = blockIdx.x;
+    if (a.nd > 1 && b >= a.d[0].blocks)
+        reduce_block(a.d[1], b - a.d[0].blocks, red);
+    else
+        reduce_block(a.d[0], b, red);
 }
 
 // --------------------------------------------------------------------------- weight packing
@@ -1343,14 +1534,89 @@ int64_t wgrad_max_chunks(int64_t RP) {
     return c < 1 ? 1 : c;
 }
 
+RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* dscale_part, int ntiles,
+                 float* grads) {
+    RedDesc d;
+    d.part = part;
+    d.dsp = dscale_part;
+    d.grads = grads;
+    d.G = grad_G(m);
+    d.nchunks = nchunks;
+    d.ntiles = ntiles;
+    d.NS = m->has_norm ? m->out_dim : 0;
+    d.blocks = (int32_t)(cdiv64(d.G, 64) + d.NS);
+    return d;
+}
+
+int launch_reduce2(const RedDesc* d, int nd, hipStream_t st) {
+    RedArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nd = nd;
+    unsigned blocks = 0;
+    for (int i = 0; i < nd; ++i) {
+        a.d[i] = d[i];
+        blocks += (unsigned)d[i].blocks;
+    }
+    ProfScope ps(PROF_WGRAD_REDUCE, st);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
 int launch_reduce(const mgn_mlp* m, const float* part, int nchunks, const float* dscale_part, int ntiles,
                   float* grads, hipStream_t st) {
-    ProfScope ps(PROF_WGRAD_REDUCE, st);
-    const int64_t G = grad_G(m);
-    const int NS = m->has_norm ? m->out_dim : 0;
-    const unsigned blocks = (unsigned)(cdiv64(G, 64) + NS);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, part, nchunks, G, dscale_part,
-                       ntiles, NS, grads);
+    const RedDesc d = red_desc(m, part, nchunks, dscale_part, ntiles, grads);
+    return launch_reduce2(&d, 1, st);
+}
+
+// ring-kernel form of a single-MLP job list (bf16, h=128): every R8 job spans a full 128-column
+// block, re-gathered inputs are plain rows (no index). false: not eligible (generic kernel).
+bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
+    constexpr int H = 128;
+    if (a.H != H || a.M <= 0 || a.rows_per_chunk % RG_RS != 0 || nj > 12) return false;
+    memset(&r, 0, sizeof(r));
+    r.njobs = nj;
+    for (int j = 0; j < nj; ++j) {
+        const WgJob& jb = a.job[j];
+        RgJob& q = r.job[j];
+        const int col0 = jb.kb * H;
+        if (jb.staged) {
+            int s = 0;
+            while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
+            const SrcSeg& g = a.seg[s];
+            if (g.idx != nullptr || g.ld % 8 != 0 || g.ld == 0) return false;
+            q.x = reinterpret_cast<const __bf16*>(g.p) + (col0 - g.coff);
+            q.ld = g.ld;
+        } else {
+            if (col0 + H > jb.kp) return false;
+            q.x = reinterpret_cast<const __bf16*>(a.act8) + jb.act_off + (int64_t)col0 * 8;
+            q.ld = 0;
+        }
+        q.z = reinterpret_cast<const __bf16*>(a.dz8) + (int64_t)jb.zl * a.RP * H;
+        q.RP = a.RP;
+        q.M = a.M;
+        q.part = a.part;
+        q.G = a.G;
+        q.w_off = jb.w_off;
+        q.b_off = jb.b_off;
+        q.n = jb.n;
+        q.k = jb.k;
+        q.kp = jb.kp;
+        q.col0 = col0;
+        q.rows_per_chunk = a.rows_per_chunk;
+        q.nchunks = nchunks;
+        q.wg0 = j * nchunks;
+    }
+    return true;
+}
+
+int launch_ring(const RgArgs& r, hipStream_t st) {
+    if (int e = set_lds((const void*)wgrad_ring_kernel, RG_LDS)) return e;
+    int wgs = 0;
+    for (int j = 0; j < r.njobs; ++j) wgs = r.job[j].wg0 + r.job[j].nchunks > wgs ? r.job[j].wg0 + r.job[j].nchunks : wgs;
+    if (wgs == 0) return 0;
+    ProfScope ps(PROF_WGRAD, st);
+    hipLaunchKernelGGL(wgrad_ring_kernel, dim3(wgs), dim3(512), RG_LDS, st, r);
     MGN_LAUNCH_CHECK();
     return 0;
 }
@@ -1358,6 +1624,13 @@ int launch_reduce(const mgn_mlp* m, const float* part, int nchunks, const float*
 template <class T, int H>
 int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
     a.njobs = nj;
+    if constexpr (sizeof(T) == 2 && H == 128) {
+        RgArgs r;
+        if (ring_jobs_from(a, nj, nchunks, r)) {
+            if (nchunks > 0 && nj > 0) return launch_ring(r, st);
+            return 0;
+        }
+    }
     auto fn = mlp_wgrad_kernel<T, H>;
     const size_t lds = wgrad_lds_bytes<T, H>(a.gathered != 0);
     if (int e = set_lds((const void*)fn, wgrad_lds_bytes<T, H>(true))) return e;
@@ -1456,6 +1729,120 @@ int launch_wgrad_proj(const mgn_mlp* m, int64_t N, const void* dP8, const void* 
 }
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// All weight gradients of a GraphNetBlock (bf16, h=128, chained path) in ONE ring launch — the
+// edge MLP over edge rows (e block of W0 + layers 1-3), the node MLP over node rows ([x ‖ aggr]
+// blocks of W0 + layers 1-3), and the x blocks of the edge W0 over node rows (dP_i/dP_j, into the
+// edge MLP's slabs) — then ONE reduction of both MLPs' slabs. Rows per workgroup are balanced over
+// all 11 jobs so the grid is about one workgroup per CU.
+struct BlockWgradIn {
+    int64_t E, N;
+    const void *e, *x, *aggr;
+    const void *eact, *edz8, *dP8;
+    const float* edsp;
+    int entiles;
+    float *epart, *egrads;
+    const void *nact, *ndz8;
+    const float* ndsp;
+    int nntiles;
+    float *npart, *ngrads;
+};
+
+int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradIn& in, hipStream_t st) {
+    constexpr int H = 128;
+    const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
+    auto rows_for = [](int64_t RP, int64_t target, int* nch) {
+        int64_t c = cdiv64(RP, target);
+        const int64_t cmax = wgrad_max_chunks(RP);
+        if (c > cmax) c = cmax;
+        if (c < 1) c = 1;
+        int64_t r = cdiv64(cdiv64(RP, c), 64) * 64;
+        *nch = (int)cdiv64(RP, r);
+        return (int)r;
+    };
+    // one round of workgroups: 4 edge + 2 projection jobs on ce chunks, 5 node jobs on cn chunks with
+    // cn/ce ≈ RPN/RPE (equal rows per workgroup), 6·ce + 5·cn <= CUs
+    const int cus = device_cus();
+    int64_t ce0 = (int64_t)((double)cus / (6.0 + 5.0 * (double)RPN / (double)RPE));
+    if (ce0 < 1) ce0 = 1;
+    int ce, cn, cp;
+    int re = 0, rn = 0;
+    for (;; --ce0) {
+        re = rows_for(RPE, cdiv64(RPE, ce0), &ce);
+        rn = rows_for(RPN, re, &cn);
+        if (6 * ce + 5 * cn <= cus || ce0 == 1) break;
+    }
+    const int rp = (int)(cdiv64(cdiv64(RPN, ce), 64) * 64);  // the projections fill the edge slabs
+    (void)cp;
+    RgArgs r;
+    memset(&r, 0, sizeof(r));
+    int nj = 0, wg = 0;
+    auto add = [&](const void* z, const void* xs, int64_t ld, int64_t RP, int64_t M, float* part, int64_t G,
+                   int64_t w_off, int64_t b_off, int n, int k, int kp, int col0, int rows, int nch) {
+        RgJob& q = r.job[nj++];
+        q.z = z;
+        q.x = xs;
+        q.ld = ld;
+        q.RP = RP;
+        q.M = M;
+        q.part = part;
+        q.G = G;
+        q.w_off = w_off;
+        q.b_off = b_off;
+        q.n = n;
+        q.k = k;
+        q.kp = kp;
+        q.col0 = col0;
+        q.rows_per_chunk = rows;
+        q.nchunks = nch;
+        q.wg0 = wg;
+        wg += nch;
+    };
+    const __bf16* edz = reinterpret_cast<const __bf16*>(in.edz8);
+    const __bf16* ndz = reinterpret_cast<const __bf16*>(in.ndz8);
+    const __bf16* dP = reinterpret_cast<const __bf16*>(in.dP8);
+    const int64_t Ge = grad_G(edge), Gn = grad_G(node);
+    // edge MLP over edge rows (heaviest first: dispatch order)
+    int64_t off = 0;
+    for (int l = 0; l < edge->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*edge, l, &n, &k);
+        const __bf16* z = edz + (int64_t)l * RPE * H;
+        if (l == 0)
+            add(z, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0, re, ce);
+        else
+            add(z, reinterpret_cast<const __bf16*>(in.eact) + act_off(*edge, in.E, l, 1), 0, RPE, in.E, in.epart, Ge,
+                off, off + (int64_t)n * k, n, k, act_cols(*edge, l), 0, re, ce);
+        off += (int64_t)n * k + n;
+    }
+    // node MLP over node rows
+    off = 0;
+    for (int l = 0; l < node->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*node, l, &n, &k);
+        const __bf16* z = ndz + (int64_t)l * RPN * H;
+        if (l == 0) {
+            add(z, in.x, H, RPN, in.N, in.npart, Gn, off, off + (int64_t)n * k, n, k, k, 0, rn, cn);
+            add(z, in.aggr, H, RPN, in.N, in.npart, Gn, off, -1, n, k, k, H, rn, cn);
+        } else {
+            add(z, reinterpret_cast<const __bf16*>(in.nact) + act_off(*node, in.N, l, 1), 0, RPN, in.N, in.npart, Gn,
+                off, off + (int64_t)n * k, n, k, act_cols(*node, l), 0, rn, cn);
+        }
+        off += (int64_t)n * k + n;
+    }
+    // x blocks of the edge W0 over node rows, into the edge slabs (chunks past N write zeros)
+    for (int s2 = 0; s2 < 2; ++s2)
+        add(dP + (int64_t)s2 * RPN * H, in.x, H, RPN, in.N, in.epart, Ge, 0, -1, H, edge->in_dim, edge->in_dim,
+            (1 + s2) * H, rp, ce);
+    r.njobs = nj;
+    if (int e2 = launch_ring(r, st)) return e2;
+    RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
+                    red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
+    (void)re;
+    return launch_reduce2(d, 2, st);
+}
+
+
 
 size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
@@ -1879,8 +2266,11 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
                        saved->aggr, st);
 }
 
+// mlp: edge MLP backward workspace (generic path: shared with the node MLP's, used in sequence);
+// nmlp: the node MLP's own (chained path: its dZ saves and slabs live until the block's single
+// weight-gradient launch at the end)
 struct BlockWs {
-    size_t mlp, dxpart, daggr, dz0, dP8, total;
+    size_t mlp, nmlp, dxpart, daggr, dz0, dP8, total;
 };
 
 static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
@@ -1893,6 +2283,8 @@ static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const 
     size_t o = 0;
     w.mlp = o;
     o += align_up(mlp_ws);
+    w.nmlp = o;
+    o += align_up(nws);
     w.dxpart = o;
     o += align_up((size_t)t->num_nodes * H * es);
     w.daggr = o;
@@ -1924,7 +2316,6 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     void* d_aggr = w + wl.daggr;
     void* dz0 = w + wl.dz0;
     void* dP8 = w + wl.dP8;
-    const size_t mlp_ws_bytes = wl.dxpart - wl.mlp;
 
     // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
     MlpIn nin;
@@ -1937,29 +2328,31 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     on.mode = MODE_NODE;
     on.o1 = dx_part;
     on.o2 = d_aggr;
-    if (chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) && t->num_nodes > 0) {
-        // chained data gradients, then the node MLP's weight gradients on the same workspace carve
+    const bool chained = chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) &&
+                         t->num_nodes > 0 && t->num_edges > 0;
+    void* ndz = nullptr;
+    float* ndsp = nullptr;
+    float* npart = nullptr;
+    int nparts = 0;
+    if (chained) {
+        // chained data gradients; the node MLP's weight gradients join the block's single ring launch
         const int64_t Nn = t->num_nodes;
-        MGN_REQUIRE(mlp_ws_bytes >= mlp_bwd_ws(node, Nn), "backward workspace too small");
-        char* q = reinterpret_cast<char*>(mlp_ws);
-        void* ndz = q;
+        MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, Nn), "backward workspace too small");
+        char* q = w + wl.nmlp;
+        ndz = q;
         q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * 2);
-        float* ndsp = reinterpret_cast<float*>(q);
+        ndsp = reinterpret_cast<float*>(q);
         q += align_up((size_t)(rows_pad(Nn) / 16) * node->out_dim * sizeof(float));  // = mlp_bwd_ws carve
-        float* npart = reinterpret_cast<float*>(q);
-        int nparts = 0;
+        npart = reinterpret_cast<float*>(q);
         if (int r = chain16_node_backward(node, Nn, &saved->node, dx_out, ndz, ndsp, &nparts, dx_part, d_aggr, st))
             return r;
-        if (int r = mlp_wgrad_any(node, Nn, saved->node.act, ndz, ndsp, nparts, npart, node_grads, &nin, 0, nullptr,
-                                  true, st))
-            return r;
     } else if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on,
-                                         node_grads, mlp_ws, mlp_ws_bytes, st)) {
+                                         node_grads, mlp_ws, wl.nmlp - wl.mlp, st)) {
         return r;
     }
     // edge MLP data gradients: dY = de_out + d_aggr[dst] -> de = de_out + dZ0·W0a, dZ0 (row-major)
     const int64_t E = t->num_edges, N = t->num_nodes;
-    MGN_REQUIRE(mlp_ws_bytes >= mlp_bwd_ws(edge, E), "backward workspace too small");
+    MGN_REQUIRE(wl.nmlp - wl.mlp >= mlp_bwd_ws(edge, E), "backward workspace too small");
     const size_t es = dt == MGN_F32 ? 4 : 2;
     int ntiles = (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
     char* p = reinterpret_cast<char*>(mlp_ws);
@@ -1989,6 +2382,28 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
         MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, dz0, dx_part, dP8, dx, st)))
     }
     if (rc) return rc;
+    if (chained) {
+        BlockWgradIn in;
+        in.E = E;
+        in.N = N;
+        in.e = e;
+        in.x = x;
+        in.aggr = saved->aggr;
+        in.eact = saved->edge.act;
+        in.edz8 = dz8;
+        in.dP8 = dP8;
+        in.edsp = dsp;
+        in.entiles = ntiles;
+        in.epart = part;
+        in.egrads = edge_grads;
+        in.nact = saved->node.act;
+        in.ndz8 = ndz;
+        in.ndsp = ndsp;
+        in.nntiles = nparts;
+        in.npart = npart;
+        in.ngrads = node_grads;
+        return block_wgrad_ring(edge, node, in, st);
+    }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
     MlpIn ein;
     memset(&ein, 0, sizeof(ein));
