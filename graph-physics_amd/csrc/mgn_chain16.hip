@@ -34,6 +34,30 @@ constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose sc
 constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
 constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
 
+// Diagnostics (build with -DMGN_STAMPS, e.g. MGN_STAMPS=1 python __graft_entry__.py): per-phase
+// s_memtime deltas of wave 0 of workgroup 0, printed once per launch. Not in normal builds.
+#ifdef MGN_STAMPS
+#define STAMP_DECL                                                                                      \
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define STAMP(i)                                                                                        \
+    do {                                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+        unsigned long long st_t;                                                                        \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");                   \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+        st_ph[i] += st_t - st_prev;                                                                     \
+        st_prev = st_t;                                                                                 \
+    } while (0)
+#define STAMP_PRINT(name)                                                                               \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                                            \
+    printf("%s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", name, st_ph[0], st_ph[1],  \
+           st_ph[2], st_ph[3], st_ph[4], st_ph[5], st_ph[6], st_ph[7], st_ph[8], st_ph[9], st_ph[10], st_ph[11])
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_PRINT(name)
+#endif
+
 __device__ __forceinline__ f4 mfma16(const bf16x8& a, const bf16x8& b, const f4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -116,6 +140,85 @@ __device__ __forceinline__ void gemm16(f4 (&acc)[8], const __bf16* W, int l, con
         for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, l, t, s, lane), B[s], acc[t]);
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+// One layer's GEMM that also stores its B operand (= the layer's input, bf16) as R8 octets and/or
+// row-major rows through the wave's 8-row scratch, with the LDS round trips placed between the
+// k-steps so they run under the MFMAs: write octet 0 | k0 | read 0 | k1 | store 0, write octet 1 |
+// k2 | read 1 | k3 | store 1. The fences only order the wave's own scratch writes and reads.
+struct StoreDst {
+    __bf16* r8;    // R8 [RP][128] (octets 2*tile, 2*tile+1) or nullptr
+    __bf16* rows;  // row-major [M][128] (rows >= M skipped) or nullptr
+};
+
+__device__ __forceinline__ void gemm16_st(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane,
+                                          __bf16* scr, StoreDst d, int64_t tile, int64_t M) {
+    const int m = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    u32x2 rv[8];
+    u32x4 rw[2];
+    auto write = [&](int u) {
+        if ((m >> 3) == u) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const u32x4 b = __builtin_bit_cast(u32x4, B[t >> 1]);
+                const u32x2 w = (t & 1) ? u32x2{b[2], b[3]} : u32x2{b[0], b[1]};
+                *reinterpret_cast<u32x2*>(scr + (m & 7) * SLD + 16 * t + 4 * g) = w;
+            }
+        }
+    };
+    auto read = [&]() {
+        if (d.r8) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rv[q][0] = *reinterpret_cast<const unsigned*>(scr + q * SLD + 2 * lane);
+        }
+        if (d.rows) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                rw[p] = *reinterpret_cast<const u32x4*>(scr + (4 * p + (lane >> 4)) * SLD + (lane & 15) * 8);
+        }
+    };
+    auto store = [&](int u) {
+        if (d.r8) {
+            bf16x8 c0, c1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const bf16x2 p = __builtin_bit_cast(bf16x2, rv[q][0]);
+                c0[q] = p[0];
+                c1[q] = p[1];
+            }
+            __bf16* p = d.r8 + (((int64_t)tile * 2 + u) * H + 2 * lane) * 8;
+            *reinterpret_cast<bf16x8*>(p) = c0;
+            *reinterpret_cast<bf16x8*>(p + 8) = c1;
+        }
+        if (d.rows) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int64_t row = tile * TR + 8 * u + 4 * p + (lane >> 4);
+                if (row < M) *reinterpret_cast<u32x4*>(d.rows + row * H + (lane & 15) * 8) = rw[p];
+            }
+        }
+    };
+    auto kstep = [&](int s) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, l, t, s, lane), B[s], acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    write(0);
+    kstep(0);
+    lds_fence();
+    read();
+    kstep(1);
+    store(0);
+    lds_fence();  // octet 0's reads are back before octet 1 overwrites the scratch
+    write(1);
+    kstep(2);
+    lds_fence();
+    read();
+    kstep(3);
+    store(1);
+    lds_fence();  // scratch free for the next user
 }
 
 __device__ __forceinline__ void to_operand(const f4 (&v)[8], bf16x8 (&B)[4]) {
@@ -229,6 +332,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     const int64_t stride = (int64_t)gridDim.x * NW;
     int64_t tile = (int64_t)blockIdx.x * NW + wave;
     const int64_t last = a.ntiles - 1;
+    STAMP_DECL;
     In16 nxt;
     int di, dj;
     load_idx(a, min(tile, last), lane, di, dj);
@@ -241,6 +345,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
     pin(di);
     pin(dj);
+    STAMP(0);
     for (; tile < a.ntiles; tile += stride) {
         const In16 in = nxt;
         // node projections of this tile (b0 folded into P_i); the layer-0 GEMM covers their latency
@@ -260,9 +365,14 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         const int64_t row = tile * TR + m;
         f4 acc[8];
         bf16x8 B[4];
+        STAMP(1);
 #pragma unroll
         for (int l = 0; l < 3; ++l) {
-            gemm16(acc, W, l, l == 0 ? in.eb : B, lane);
+            if (l == 0)
+                gemm16(acc, W, 0, in.eb, lane);
+            else
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
+            STAMP(2);
             unsigned bits = 0u;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -276,10 +386,11 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
             }
             to_operand(acc, B);
             a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
-            store_r8(acc, scr, a.act8 + a.act_off[l + 1], tile, lane);
+            STAMP(3);
         }
-        // layer 3 + RMSNorm + residual
-        gemm16(acc, W, 3, B, lane);
+        // layer 3 (stores its input, the R8 save of layer 3) + RMSNorm + residual
+        gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+        STAMP(4);
         float ss = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -297,6 +408,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         const float rq = __builtin_amdgcn_rcpf(q);  // bf16 outputs: z·(1/q) is within 2 fp32 ulp of z/q
         if (g == 0 && row < a.M) a.rden_save[row] = q;
         store_rows(acc, scr, a.z_save, tile, a.M, lane);
+        STAMP(5);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
@@ -305,13 +417,16 @@ __global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
                 acc[t][r] = fmaf(s[r], acc[t][r] * rq, (float)in.eb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
+        STAMP(6);
 #pragma unroll
         for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
         pin(ndi);
         pin(ndj);
         di = ndi;
         dj = ndj;
+        STAMP(7);
     }
+    STAMP_PRINT("fwd16");
 }
 
 // ------------------------------------------------------------------------------------ backward
@@ -368,6 +483,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     const int64_t stride = (int64_t)gridDim.x * NW;
     int64_t tile = (int64_t)blockIdx.x * NW + wave;
     const int64_t last = a.ntiles - 1;
+    STAMP_DECL;
     const int gi0 = bidx(a, min(tile, last), lane);
     stage16(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
@@ -383,6 +499,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         pin_in(nxt);
         pin(ngi);
     }
+    STAMP(0);
     for (; tile < a.ntiles; tile += stride) {
         const int64_t row = tile * TR + m;
         const bool ok = row < a.M;
@@ -420,11 +537,12 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         unsigned mcur[3];
 #pragma unroll
         for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
+        STAMP(1);
         bload(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
         bf16x8 B[4];
         to_operand(acc, B);
-        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
+        STAMP(2);
         // layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_l > 0]
         u32x2 dre[8];  // de_out of this tile again (cache-hot), for the layer-0 residual
 #pragma unroll
@@ -434,7 +552,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
                 for (int t = 0; t < 8; ++t) dre[t] = *reinterpret_cast<const u32x2*>(d + 16 * t);
             }
-            gemm16(acc, W, l, B, lane);
+            // stores its B operand dZ_l (R8) under the MFMAs
+            gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
+            STAMP(3);
             const unsigned bw = mcur[l - 1];
 #pragma unroll
             for (int t = 0; t < 8; ++t)
@@ -442,18 +562,21 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
                 for (int r = 0; r < 4; ++r)
                     acc[t][r] = __int_as_float(__float_as_int(acc[t][r]) & bit_sel(bw, 4 * t + r));
             to_operand(acc, B);
-            store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
-            if (l == 1) store_rows(acc, scr, a.dz0, tile, a.M, lane);
+            STAMP(4);
         }
-        // layer 0, e block: de = de_out + dZ0 · W0a
-        gemm16(acc, W, 0, B, lane);
+        // layer 0, e block: de = de_out + dZ0 · W0a (stores dZ0 as R8 and row-major under the MFMAs)
+        gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, a.dz0}, tile, a.M);
+        STAMP(6);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] += bf4(dre[t]);
         store_rows(acc, scr, a.de, tile, a.M, lane);
+        STAMP(7);
         pin_in(nxt);
         pin(ngi2);
         ngi = ngi2;
+        STAMP(8);
     }
+    STAMP_PRINT("bwd16");
     // dscale partials of the workgroup: the waves' rows in wave order
     __syncthreads();
     if (threadIdx.x < H) {
