@@ -72,14 +72,22 @@ __device__ __forceinline__ f4 bf4(u32x2 v) {
     return f4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
 }
 
-// sum over the 16 lanes of a DPP row (lanes 16g .. 16g+15), result in every lane of the row:
-// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror
-__device__ __forceinline__ float row16_sum(float v) {
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
-    return v;
+// the 4 components of v summed over the 16 lanes of a DPP row, transposing as it goes: lane m
+// returns the total of component 2(m&1) + ((m>>1)&1) (pairs m^1 trade two components, pairs m^2
+// one, then rotations by 4 and 8 add the four lanes holding the same component): 6 DPP adds for
+// four sums instead of 16
+__device__ __forceinline__ float row16_sum4(const f4& v, int m) {
+    const bool odd = m & 1, b1 = (m >> 1) & 1;
+    const float s0 = odd ? v[0] : v[2], s1 = odd ? v[1] : v[3];
+    float k0 = odd ? v[2] : v[0], k1 = odd ? v[3] : v[1];
+    k0 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xF, 0xF, false));
+    k1 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xF, 0xF, false));
+    const float sb = b1 ? k0 : k1;
+    float k = b1 ? k1 : k0;
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(sb), 0x4E, 0xF, 0xF, false));
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(k), 0x124, 0xF, 0xF, false));  // row_ror:4
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(k), 0x128, 0xF, 0xF, false));  // row_ror:8
+    return k;
 }
 
 __device__ __forceinline__ int64_t clamp_row(int64_t row, int64_t M) { return row < M ? row : M - 1; }
@@ -480,6 +488,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
     float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
     const int m = lane & 15, g = lane >> 4;
+    const int r4 = 2 * (m & 1) + ((m >> 1) & 1);  // row16_sum4's component in lane m
     const int64_t stride = (int64_t)gridDim.x * NW;
     int64_t tile = (int64_t)blockIdx.x * NW + wave;
     const int64_t last = a.ntiles - 1;
@@ -530,9 +539,10 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const float dy = acc[t][r];
                 acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
-                ds[r] = row16_sum(ok ? dy * z[r] * rq : 0.f);
+                ds[r] = ok ? dy * z[r] * rq : 0.f;
             }
-            if (m == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * t + 4 * g) += ds;
+            const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
+            if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
         }
         unsigned mcur[3];
 #pragma unroll
@@ -746,6 +756,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
     float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
     const int m = lane & 15, g = lane >> 4;
+    const int r4 = 2 * (m & 1) + ((m >> 1) & 1);  // row16_sum4's component in lane m
     stage16(W, a.wtpack, a.woff, a.wks, true);
     for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
     for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
@@ -793,9 +804,10 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             for (int r = 0; r < 4; ++r) {
                 const float dy = acc[t][r];
                 acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
-                ds[r] = row16_sum(ok ? dy * z[r] * rq : 0.f);
+                ds[r] = ok ? dy * z[r] * rq : 0.f;
             }
-            if (m == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * t + 4 * g) += ds;
+            const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
+            if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
         }
         bf16x8 B[4];
         to_operand(acc, B);
