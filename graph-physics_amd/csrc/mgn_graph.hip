@@ -165,13 +165,166 @@ __global__ __launch_bounds__(256) void colstats_partial(const float* __restrict_
     }
 }
 
-__global__ __launch_bounds__(64) void colstats_final(const float* __restrict__ part, int nblocks, int cols,
-                                                     float* __restrict__ out) {
-    const int i = threadIdx.x;
-    if (i >= 2 * cols) return;
+// Σ_b part[b][i] over nblocks <= 256 partial rows by one wave: lane-strided partials, then a fixed
+// xor butterfly (every lane ends with the same total; deterministic).
+__device__ __forceinline__ float partial_total(const float* __restrict__ part, int nblocks, int cols, int i,
+                                               int lane) {
     float t = 0.f;
-    for (int b = 0; b < nblocks; ++b) t += part[(int64_t)b * 2 * cols + i];
-    out[i] = t;
+    for (int b = lane; b < nblocks; b += 64) t += part[(int64_t)b * 2 * cols + i];
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) t += __shfl_xor(t, w);
+    return t;
+}
+
+// the 2*cols totals, one wave per output (4 waves)
+__global__ __launch_bounds__(256) void colstats_final(const float* __restrict__ part, int nblocks, int cols,
+                                                      float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x >> 6; i < 2 * cols; i += 4) {
+        const float t = partial_total(part, nblocks, cols, i, lane);
+        if (lane == 0) out[i] = t;
+    }
+}
+
+// Normalizer.forward (reference layers.py:265-392): one block finishes the batch column sums
+// (same block order as colstats_final) or takes the caller's pending {Σx, Σx², count}, applies
+// _accumulate to the module's fp32 buffers exactly as the torch expressions do (acc += live ? s : 0,
+// live = num_acc < max_acc), and leaves mean / max(sqrt(max(var, 0)), eps) per column in mstd for
+// the elementwise pass.
+__global__ __launch_bounds__(256) void normalizer_update(const float* __restrict__ part, int nblocks, int cols,
+                                                        const float* __restrict__ pending, float rows_f,
+                                                        int accumulate, float* acc_sum, float* acc_sum_sq,
+                                                        float* acc_count, float* num_acc, float max_acc, float eps,
+                                                        float* __restrict__ mstd) {
+#pragma clang fp contract(off)  // one rounding per torch op: no fused multiply-adds here
+    __shared__ float tot[2 * 32];
+    const int i = threadIdx.x;
+    const float count_old = *acc_count, num_old = *num_acc;
+    if (accumulate && !pending)
+        for (int o = threadIdx.x >> 6; o < 2 * cols; o += 4) {
+            const float t = partial_total(part, nblocks, cols, o, threadIdx.x & 63);
+            if ((threadIdx.x & 63) == 0) tot[o] = t;
+        }
+    __syncthreads();  // totals in LDS; every thread has read the old scalars before thread 0 writes them
+    const bool live = accumulate && num_old < max_acc;
+    float cnt = 0.f;
+    if (accumulate) cnt = pending ? pending[2 * cols] : rows_f;
+    const float count_new = count_old + (live ? cnt : 0.f);
+    if (i < cols) {
+        float sm = acc_sum[i], sq = acc_sum_sq[i];
+        if (accumulate) {
+            float s = 0.f, s2 = 0.f;
+            if (pending) {
+                s = pending[i];
+                s2 = pending[cols + i];
+            } else {
+                s = tot[i];
+                s2 = tot[cols + i];
+            }
+            sm = sm + (live ? s : 0.f);
+            sq = sq + (live ? s2 : 0.f);
+            acc_sum[i] = sm;
+            acc_sum_sq[i] = sq;
+        }
+        const float c1 = count_new < 1.f ? 1.f : count_new;  // clamp(min=1)
+        const float mean = sm / c1;
+        const float var = sq / c1 - mean * mean;
+        const float sd = sqrtf(var < 0.f ? 0.f : var);
+        mstd[i] = mean;
+        mstd[cols + i] = sd != sd ? sd : (sd < eps ? eps : sd);  // torch.max: NaN propagates
+    }
+    if (i == 0 && accumulate) {
+        *acc_count = count_new;
+        *num_acc = num_old + (live ? 1.f : 0.f);
+    }
+}
+
+__global__ __launch_bounds__(256) void normalizer_apply(const float* __restrict__ x, int64_t rows, int cols,
+                                                        int64_t ld, const float* __restrict__ mstd,
+                                                        float* __restrict__ out) {
+#pragma clang fp contract(off)
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= rows * cols) return;
+    const int64_t r = k / cols;
+    const int c = (int)(k - r * cols);
+    out[k] = (x[r * ld + c] - mstd[c]) / mstd[cols + c];
+}
+
+// Masked L2 loss (reference utils/loss.py:10-65 in its masked_mse form): one block, rows strided
+// over the threads, fixed-order tree: deterministic.
+__device__ __forceinline__ float type_mask_of(const float* nt, int64_t ld, int64_t r, unsigned tmask) {
+    const float v = nt[r * ld];
+    const int t = (int)v;
+    return (v == (float)t && t >= 0 && t < 32 && ((tmask >> t) & 1u)) ? 1.f : 0.f;
+}
+
+// partial sums per block (fixed row range, strided threads, LDS tree) -> part[block] = {Σ m·err, Σ m}
+constexpr int MSE_BLOCKS = 64;
+__global__ __launch_bounds__(256) void masked_mse_partial(const float* __restrict__ pred,
+                                                          const float* __restrict__ tgt, int64_t rows, int cols,
+                                                          const float* __restrict__ nt, int64_t nt_ld,
+                                                          unsigned tmask, int64_t rows_per_block,
+                                                          float* __restrict__ part) {
+    __shared__ float ra[256], rc[256];
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+    float acc = 0.f, cnt = 0.f;
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+        const float m = type_mask_of(nt, nt_ld, r, tmask);
+        float e = 0.f;
+        for (int c = 0; c < cols; ++c) {
+            const float d = pred[r * cols + c] - tgt[r * cols + c];
+            e += d * d;
+        }
+        acc += m * e;
+        cnt += m;
+    }
+    ra[threadIdx.x] = acc;
+    rc[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            ra[threadIdx.x] += ra[threadIdx.x + w];
+            rc[threadIdx.x] += rc[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = ra[0];
+        part[2 * blockIdx.x + 1] = rc[0];
+    }
+}
+
+__global__ __launch_bounds__(64) void masked_mse_final(const float* __restrict__ part, int nblocks, int cols,
+                                                       const float* count_dev, float* loss, float* count_out) {
+    const int lane = threadIdx.x;
+    float a = 0.f, c = 0.f;
+    for (int b = lane; b < nblocks; b += 64) {
+        a += part[2 * b];
+        c += part[2 * b + 1];
+    }
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        a += __shfl_xor(a, w);
+        c += __shfl_xor(c, w);
+    }
+    if (lane == 0) {
+        const float cc = count_dev ? *count_dev : c;
+        *loss = a / (cc * (float)cols);
+        if (count_out) *count_out = cc;
+    }
+}
+
+__global__ __launch_bounds__(256) void masked_mse_bwd(const float* __restrict__ pred, const float* __restrict__ tgt,
+                                                      int64_t rows, int cols, const float* __restrict__ nt,
+                                                      int64_t nt_ld, unsigned tmask, const float* count,
+                                                      const float* gout, float* __restrict__ grad) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= rows * cols) return;
+    const int64_t r = k / cols;
+    const float m = type_mask_of(nt, nt_ld, r, tmask);
+    const float scale = (gout ? *gout : 1.f) / (*count * (float)cols);
+    grad[k] = m != 0.f ? scale * (2.f * (pred[k] - tgt[k])) : 0.f;
 }
 
 extern "C" {
@@ -304,7 +457,73 @@ int mgn_column_stats(const float* x, int64_t rows, int32_t cols, int64_t ld, flo
     float* part = reinterpret_cast<float*>(ws);
     hipLaunchKernelGGL(colstats_partial, dim3(nb), dim3(256), 0, st, x, rows, (int)cols, ld, rpb, part);
     MGN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colstats_final, dim3(1), dim3(64), 0, st, (const float*)part, nb, (int)cols, sums);
+    hipLaunchKernelGGL(colstats_final, dim3(1), dim3(256), 0, st, (const float*)part, nb, (int)cols, sums);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+size_t mgn_normalizer_workspace_bytes(int64_t rows, int32_t cols) {
+    return mgn_column_stats_workspace_bytes(rows, cols) + 256;
+}
+
+int mgn_normalizer_forward(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t accumulate,
+                           const float* pending, float* acc_sum, float* acc_sum_sq, float* acc_count, float* num_acc,
+                           float max_acc, float eps, float* out, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    MGN_REQUIRE(cols >= 1 && cols <= STAT_MAXC, "normalizer: cols must be in [1, 32]");
+    MGN_REQUIRE(ld >= cols, "normalizer: ld < cols");
+    MGN_REQUIRE(ws_bytes >= mgn_normalizer_workspace_bytes(rows, cols), "normalizer: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    float* mstd = reinterpret_cast<float*>(ws);  // [2 * cols] (256 B)
+    float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + 256);
+    int nb = 0;
+    if (accumulate && !pending && rows > 0) {
+        int64_t rpb = cdiv64(rows, STAT_BLOCKS);
+        if (rpb < 256) rpb = 256;
+        nb = (int)cdiv64(rows, rpb);
+        hipLaunchKernelGGL(colstats_partial, dim3(nb), dim3(256), 0, st, x, rows, (int)cols, ld, rpb, part);
+        MGN_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(normalizer_update, dim3(1), dim3(256), 0, st, (const float*)part, nb, (int)cols, pending,
+                       (float)rows, (int)accumulate, acc_sum, acc_sum_sq, acc_count, num_acc, max_acc, eps, mstd);
+    MGN_LAUNCH_CHECK();
+    if (rows * cols > 0) {
+        hipLaunchKernelGGL(normalizer_apply, dim3((unsigned)cdiv64(rows * cols, 256)), dim3(256), 0, st, x, rows,
+                           (int)cols, ld, (const float*)mstd, out);
+        MGN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+size_t mgn_masked_mse_workspace_bytes(int64_t rows) {
+    (void)rows;
+    return 2 * MSE_BLOCKS * sizeof(float);
+}
+
+int mgn_masked_mse(const float* pred, const float* target, int64_t rows, int32_t cols, const float* node_type,
+                   int64_t nt_ld, uint32_t type_mask, const float* count, float* loss, float* count_out, void* ws,
+                   size_t ws_bytes, mgn_stream_t stream) {
+    MGN_REQUIRE(cols >= 1, "masked_mse: cols must be >= 1");
+    MGN_REQUIRE(ws_bytes >= mgn_masked_mse_workspace_bytes(rows), "masked_mse: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    float* part = reinterpret_cast<float*>(ws);
+    int64_t rpb = cdiv64(rows > 0 ? rows : 1, MSE_BLOCKS);
+    if (rpb < 256) rpb = 256;
+    const int nb = (int)cdiv64(rows > 0 ? rows : 1, rpb);
+    hipLaunchKernelGGL(masked_mse_partial, dim3(nb), dim3(256), 0, st, pred, target, rows, (int)cols, node_type,
+                       nt_ld, type_mask, rpb, part);
+    MGN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(masked_mse_final, dim3(1), dim3(64), 0, st, (const float*)part, nb, (int)cols, count, loss,
+                       count_out);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int mgn_masked_mse_backward(const float* pred, const float* target, int64_t rows, int32_t cols,
+                            const float* node_type, int64_t nt_ld, uint32_t type_mask, const float* count,
+                            const float* grad_loss, float* grad, mgn_stream_t stream) {
+    if (rows * cols == 0) return 0;
+    hipLaunchKernelGGL(masked_mse_bwd, dim3((unsigned)cdiv64(rows * cols, 256)), dim3(256), 0, (hipStream_t)stream,
+                       pred, target, rows, (int)cols, node_type, nt_ld, type_mask, count, grad_loss, grad);
     MGN_LAUNCH_CHECK();
     return 0;
 }

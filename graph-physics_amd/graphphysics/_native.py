@@ -20,6 +20,8 @@ _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _sz = ctypes.c_size_t
 _dbl = ctypes.c_double
+_f32 = ctypes.c_float
+_u32 = ctypes.c_uint32
 
 
 class Topology(ctypes.Structure):
@@ -73,6 +75,12 @@ EXPORTS = {
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),
     "mgn_column_stats": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _sz, _vp]),
+    "mgn_normalizer_workspace_bytes": (_sz, [_i64, _i32]),
+    "mgn_normalizer_forward": (_i32, [_vp, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp,
+                                      _vp, _sz, _vp]),
+    "mgn_masked_mse_workspace_bytes": (_sz, [_i64]),
+    "mgn_masked_mse": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
     "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
     "mgn_profile_enable": (_i32, [_i32]),
@@ -175,3 +183,23 @@ def column_stats(x):
     check(lib().mgn_column_stats(ptr(x), rows, cols, x.stride(0), ptr(out), ptr(ws), ws.numel(),
                                  stream_ptr(x.device)))
     return out[:cols].view(1, cols), out[cols:].view(1, cols)
+
+
+def normalizer_forward(x, accumulate, pending, acc_sum, acc_sum_sq, acc_count, num_acc, max_acc, eps):
+    """Normalizer.forward on libmgn (mgn_normalizer_forward): updates the fp32 buffers in place when
+    accumulating and returns (x - mean) / std as a new contiguous fp32 tensor. pending: None or a
+    float32 [2*cols + 1] device tensor {Σx, Σx², count}."""
+    import torch
+
+    require_device(x)
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1:
+        x = x.float().contiguous()
+    rows, cols = x.shape
+    out = torch.empty((rows, cols), dtype=torch.float32, device=x.device)
+    ws = torch.empty(max(int(lib().mgn_normalizer_workspace_bytes(rows, cols)), 4), dtype=torch.uint8,
+                     device=x.device)
+    check(lib().mgn_normalizer_forward(ptr(x), rows, cols, x.stride(0), int(bool(accumulate)),
+                                       ptr(pending) if pending is not None else None, ptr(acc_sum),
+                                       ptr(acc_sum_sq), ptr(acc_count), ptr(num_acc), float(max_acc),
+                                       float(eps), ptr(out), ptr(ws), ws.numel(), stream_ptr(x.device)))
+    return out

@@ -78,6 +78,8 @@ class Normalizer(nn.Module):
                              torch.zeros((1, size), dtype=torch.float32, device=device))
         self.process_group = None
         self._pending = None  # (sum, sum_sq, count) of the global batch, set by set_pending()
+        self._pending_packed = None  # the same three as one [2*size + 1] tensor (views above)
+        self._eps_cache = None
 
     def batch_statistics(self, d: torch.Tensor):
         """(Σ rows, Σ rows², row count) of one local batch (no exchange)."""
@@ -95,16 +97,40 @@ class Normalizer(nn.Module):
         computing and exchanging its own: lets a data-parallel step exchange them before a replayed
         hipGraph. The buffers are static, so a captured forward reads each step's values."""
         if self._pending is None:
-            self._pending = (s.detach().clone(), s2.detach().clone(), cnt.detach().clone().reshape(()))
-        else:
-            self._pending[0].copy_(s)
-            self._pending[1].copy_(s2)
-            self._pending[2].copy_(cnt.reshape(()))
+            k = s.numel()
+            packed = torch.empty(2 * k + 1, dtype=torch.float32, device=s.device)
+            self._pending_packed = packed
+            self._pending = (packed[:k].view_as(s), packed[k:2 * k].view_as(s2), packed[2 * k])
+        self._pending[0].copy_(s)
+        self._pending[1].copy_(s2)
+        self._pending[2].copy_(cnt.reshape(()))
 
     def clear_pending(self):
         self._pending = None
+        self._pending_packed = None
+
+    def _eps(self) -> float:
+        t = self._std_epsilon
+        if self._eps_cache is None or self._eps_cache[0] is not t:
+            self._eps_cache = (t, float(t))
+        return self._eps_cache[1]
+
+    def _native_ok(self, d: torch.Tensor, accumulate: bool) -> bool:
+        if not (d.is_cuda and d.dim() == 2 and 1 <= d.shape[1] <= 32 and not d.requires_grad):
+            return False
+        if accumulate and self.process_group is not None and self._pending is None:
+            return False  # statistics exchanged inside _accumulate: torch path
+        bufs = (self._acc_sum, self._acc_sum_squared, self._acc_count, self._num_accumulations)
+        return all(b.dtype == torch.float32 and b.is_contiguous() and b.device == d.device for b in bufs)
 
     def forward(self, batched_data: torch.Tensor, accumulate: bool = True) -> torch.Tensor:
+        if self._native_ok(batched_data, accumulate):
+            from graphphysics import _native as nat  # one native pass: statistics, _accumulate, normalise
+
+            return nat.normalizer_forward(batched_data.detach(), accumulate,
+                                          self._pending_packed if accumulate else None, self._acc_sum,
+                                          self._acc_sum_squared, self._acc_count, self._num_accumulations,
+                                          float(self._max_accumulations), self._eps())
         if accumulate:
             self._accumulate(batched_data.detach())
         return (batched_data - self._mean()) / self._std_with_epsilon()

@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 2
+#define MGN_ABI_VERSION 3
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -173,6 +173,32 @@ int mgn_segment_sum(const void* src, const int32_t* seg_ptr, int64_t segments, i
 size_t mgn_column_stats_workspace_bytes(int64_t rows, int32_t cols);
 int mgn_column_stats(const float* x, int64_t rows, int32_t cols, int64_t ld, float* sums, void* ws,
                      size_t ws_bytes, mgn_stream_t stream);
+
+/* Normalizer.forward (reference layers.py:265-392, _accumulate 333-352, _mean/_std_with_epsilon
+ * 354-369) on a row-major fp32 [rows, cols] matrix x (row stride ld), cols <= 32: when
+ * accumulate != 0 and *num_acc < max_acc, the batch statistics — column sums of x and x² and the
+ * row count, or the caller's pending = float[2*cols + 1] {Σx, Σx², count} (e.g. already summed
+ * over ranks) — are added to the module's fp32 buffers acc_sum[cols], acc_sum_sq[cols],
+ * *acc_count and *num_acc (+1); then out[rows, cols] (contiguous) = (x - mean) / max(sqrt(max(var,
+ * 0)), eps), mean = acc_sum / max(acc_count, 1), var = acc_sum_sq / max(acc_count, 1) - mean².
+ * Same fp32 expressions as the reference's torch ops (bit-identical results). */
+size_t mgn_normalizer_workspace_bytes(int64_t rows, int32_t cols);
+int mgn_normalizer_forward(const float* x, int64_t rows, int32_t cols, int64_t ld, int32_t accumulate,
+                           const float* pending, float* acc_sum, float* acc_sum_sq, float* acc_count, float* num_acc,
+                           float max_acc, float eps, float* out, void* ws, size_t ws_bytes, mgn_stream_t stream);
+
+/* Masked L2 loss (reference utils/loss.py:10-65): *loss = Σ_r m_r Σ_c (pred - target)² / (count ·
+ * cols) over row-major fp32 [rows, cols] pred/target, m_r = 1 when node_type[r·nt_ld] (a float
+ * column, e.g. a strided view of x) is an integer t < 32 with bit t of type_mask set; count =
+ * *count when given (data-parallel global count), else Σ m (written to *count_out if non-null).
+ * Backward: grad = (*grad_loss or 1) · 2 (pred - target) · m / (count · cols). Deterministic. */
+size_t mgn_masked_mse_workspace_bytes(int64_t rows);
+int mgn_masked_mse(const float* pred, const float* target, int64_t rows, int32_t cols, const float* node_type,
+                   int64_t nt_ld, uint32_t type_mask, const float* count, float* loss, float* count_out, void* ws,
+                   size_t ws_bytes, mgn_stream_t stream);
+int mgn_masked_mse_backward(const float* pred, const float* target, int64_t rows, int32_t cols,
+                            const float* node_type, int64_t nt_ld, uint32_t type_mask, const float* count,
+                            const float* grad_loss, float* grad, mgn_stream_t stream);
 
 /* torch.optim.AdamW semantics (decoupled weight decay p *= 1 - lr*wd, bias-corrected moments,
  * denominator sqrt(v)/sqrt(1-beta2^t) + eps), fp32, over n contiguous elements. */

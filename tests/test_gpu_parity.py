@@ -440,6 +440,62 @@ def test_column_stats_vs_fp64():
     assert torch.equal(a, s) and torch.equal(b, s2)  # deterministic
 
 
+def test_normalizer_native_matches_torch_ops():
+    """Normalizer.forward on libmgn (statistics + _accumulate + normalise in one call) is
+    bit-identical to the module's torch expressions (reference layers.py:265-392): outputs and all
+    four buffers, over accumulating calls, the max_accumulations cut-off, pending (exchanged)
+    statistics and a non-accumulating call."""
+    from graphphysics.models.layers import Normalizer
+
+    g = torch.Generator().manual_seed(5)
+    for cols in (2, 3, 11):
+        nat_n = Normalizer(cols, max_accumulations=3, device=DEV)
+        ref_n = Normalizer(cols, max_accumulations=3, device=DEV)
+        for it in range(5):
+            x = (torch.randn(1000 + 37 * it, cols, generator=g) * (it + 1) + it).to(DEV)
+            acc = it != 3
+            if it == 4:  # statistics handed in (data-parallel prologue)
+                s, s2, c = nat_n.batch_statistics(x)
+                nat_n.set_pending(s * 2, s2 * 2, c * 2)
+                ref_n.set_pending(s * 2, s2 * 2, c * 2)
+            out = nat_n(x, acc)
+            if acc:
+                ref_n._accumulate(x)
+            ref = (x - ref_n._mean()) / ref_n._std_with_epsilon()
+            assert torch.equal(out, ref), (cols, it)
+            for name in ("_acc_sum", "_acc_sum_squared", "_acc_count", "_num_accumulations"):
+                assert torch.equal(getattr(nat_n, name), getattr(ref_n, name)), (cols, it, name)
+        assert float(nat_n._num_accumulations) == 3.0  # cut off at max_accumulations
+
+
+def test_masked_mse_native_vs_torch():
+    """masked_mse on libmgn: loss vs an fp64 evaluation, gradient vs autograd of the torch form
+    (reference utils/loss.py:10-65), with and without an explicit (global) count."""
+    from graphphysics.utils import loss as L
+
+    g = torch.Generator().manual_seed(6)
+    rows, cols = 15384, 2
+    pred = torch.randn(rows, cols, generator=g).to(DEV).requires_grad_(True)
+    tgt = torch.randn(rows, cols, generator=g).to(DEV)
+    x = torch.randn(rows, 5, generator=g)
+    x[:, 4] = torch.randint(0, 9, (rows,), generator=g).float()
+    nt = x.to(DEV)[:, 4]  # strided column, as the simulator passes it
+    masks = [0, 5]
+    for count in (None, torch.tensor(12345.0, device=DEV)):
+        loss = L.masked_mse(tgt, pred, nt, masks, count=count)
+        gnat, = torch.autograd.grad(loss, pred)
+        m = ((nt == 0) | (nt == 5)).double()
+        c = m.sum() if count is None else count.double()
+        ref = (((pred.double() - tgt.double()) ** 2).sum(1) * m).sum() / (c * cols)
+        assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref))
+        p2 = pred.detach().clone().requires_grad_(True)
+        mt = m.float()
+        ct = mt.sum() if count is None else count
+        lt = (((p2 - tgt) ** 2).sum(1) * mt).sum() / (ct * cols)
+        gref, = torch.autograd.grad(lt, p2)
+        torch.testing.assert_close(gnat, gref, rtol=1e-5, atol=1e-10)
+
+
 def test_captured_data_parallel_step_matches_captured_step():
     """The N>1 bench step (statistics exchanged before a replayed forward+backward graph, eager
     gradient all-reduce + AdamW) run on a 1-rank RCCL group equals the single-process captured step."""
