@@ -83,6 +83,17 @@ EXPORTS = {
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
     "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+    "mgn_coalesce_workspace_bytes": (_sz, [_i64]),
+    "mgn_coalesce": (_i32, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_face_to_edge_keys": (_i64, [_i32, _i64]),
+    "mgn_face_to_edge": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_khop_count_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "mgn_khop_count": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _sz, _vp]),
+    "mgn_khop_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "mgn_khop_hop": (_i32, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_edge_features": (_i32, [_vp, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _vp, _sz, _vp]),
+    "mgn_radius_pairs_workspace_bytes": (_sz, [_i64]),
+    "mgn_radius_pairs": (_i32, [_vp, _i64, _i32, _i64, _dbl, _vp, _i64, _vp, _i64, _vp, _vp, _sz, _vp]),
     "mgn_profile_enable": (_i32, [_i32]),
     "mgn_profile_collect": (_i32, [_i32, _vp, _vp]),
 }

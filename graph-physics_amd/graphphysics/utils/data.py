@@ -11,7 +11,10 @@ except ImportError:  # pragma: no cover
 
         @property
         def num_nodes(self):
-            return self.x.size(0) if getattr(self, "x", None) is not None else None
+            for k in ("x", "pos"):
+                if getattr(self, k, None) is not None:
+                    return getattr(self, k).size(0)
+            return None
 
         def to(self, device):
             for k, v in list(vars(self).items()):

@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 3
+#define MGN_ABI_VERSION 4
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -211,6 +211,58 @@ int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
                   mgn_stream_t stream);
+
+/* ---------------------------------------------------------------- graph construction */
+/* On-device replacements for the reference's per-sample host preprocessing (SURVEY.md §8(f)
+ * rows 1 and 4). Edge lists are int64 [2, E] row-major (row block, then col block). Outputs are
+ * coalesced: sorted by (row, col), duplicates removed. These calls synchronise the stream once to
+ * return the data-dependent count to the host. Indices outside [0, num_nodes) fail with
+ * "edge_index out of range" (the reference raises from ATen). */
+#define MGN_COALESCE_SYMMETRIZE 1      /* add (col, row) for every (row, col): to_undirected */
+#define MGN_COALESCE_DROP_SELF_LOOPS 2 /* drop (i, i)                                          */
+size_t mgn_coalesce_workspace_bytes(int64_t num_keys);
+/* torch_geometric.utils.to_undirected(edge_index, num_nodes) / torch sparse coalesce() of the
+ * pattern (reference dataset/preprocessing.py:135, utils/torch_graph.py:32-36). out capacity:
+ * 2·num_keys int64, num_keys = num_edges (·2 with MGN_COALESCE_SYMMETRIZE); out[0:2E] holds the
+ * [2, E] result, *num_out = E (host). */
+int mgn_coalesce(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int32_t flags,
+                 int64_t* out, int64_t* num_out, void* ws, size_t ws_bytes, mgn_stream_t stream);
+/* T.FaceToEdge(remove_faces=False) (reference dataset/preprocessing.py:410,431): cells [k, C]
+ * int64 row-major, k = 3 (triangles: pairs (f0,f1), (f1,f2), (f0,f2)) or k = 4 (tetrahedra split
+ * into the 4 triangles of utils/torch_graph.py:173-181), then to_undirected. Workspace and out
+ * capacity from num_keys = mgn_face_to_edge_keys(k, C). */
+int64_t mgn_face_to_edge_keys(int32_t verts_per_cell, int64_t num_cells);
+int mgn_face_to_edge(const int64_t* cells, int32_t verts_per_cell, int64_t num_cells, int64_t num_nodes,
+                     int64_t* edge_index, int64_t* num_edges, void* ws, size_t ws_bytes, mgn_stream_t stream);
+/* One hop of compute_k_hop_edge_index (reference utils/torch_graph.py:38-51): the pattern of
+ * A_k + A_k·A with self loops removed, coalesced. edge_index_a = A must be coalesced (sorted by
+ * row); A_k any edge list. Two calls: mgn_khop_count returns the candidate count num_keys
+ * (= E_k + Σ_k deg_A(col_k)), then mgn_khop_hop (workspace mgn_khop_workspace_bytes, out capacity
+ * 2·num_keys) produces the result and *num_out. */
+size_t mgn_khop_count_workspace_bytes(int64_t num_edges_k, int64_t num_edges_a, int64_t num_nodes);
+int mgn_khop_count(const int64_t* edge_index_k, int64_t num_edges_k, const int64_t* edge_index_a,
+                   int64_t num_edges_a, int64_t num_nodes, int64_t* num_keys, void* ws, size_t ws_bytes,
+                   mgn_stream_t stream);
+size_t mgn_khop_workspace_bytes(int64_t num_keys, int64_t num_edges_k, int64_t num_nodes);
+int mgn_khop_hop(const int64_t* edge_index_k, int64_t num_edges_k, const int64_t* edge_index_a,
+                 int64_t num_edges_a, int64_t num_nodes, int64_t num_keys, int64_t* out, int64_t* num_out,
+                 void* ws, size_t ws_bytes, mgn_stream_t stream);
+/* T.Cartesian(norm=False) ‖ T.Distance(norm=False) (reference dataset/preprocessing.py:16-23) and
+ * add_world_pos_features (143-174): out[k, 0:dim] = pos[row_k] − pos[col_k], out[k, dim] = its
+ * L2 norm; fp32, pos row stride pos_ld, out row stride out_ld >= dim + 1, dim <= 3. ws >= 4 B. */
+int mgn_edge_features(const float* pos, int64_t pos_ld, int32_t dim, const int64_t* edge_index,
+                      int64_t num_edges, int64_t num_nodes, float* out, int64_t out_ld, void* ws,
+                      size_t ws_bytes, mgn_stream_t stream);
+/* cKDTree(pos).query_pairs(radius) of add_world_edges (reference dataset/preprocessing.py:114-121):
+ * all (i, j), i < j, with the fp64 distance <= radius, as a [2, P] int64 list in out[0:2P]
+ * (out[0:P] = i, out[P:2P] = j); pair order unspecified. node_type (float
+ * column, stride node_type_ld) non-null keeps only OBSTACLE(1)–NORMAL(0) pairs in either order
+ * (preprocessing.py:123-133). *num_pairs = P always; nothing is written when out is NULL or
+ * capacity < P (call again with capacity >= P). */
+size_t mgn_radius_pairs_workspace_bytes(int64_t num_nodes);
+int mgn_radius_pairs(const float* pos, int64_t pos_ld, int32_t dim, int64_t num_nodes, double radius,
+                     const float* node_type, int64_t node_type_ld, int64_t* out, int64_t capacity,
+                     int64_t* num_pairs, void* ws, size_t ws_bytes, mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- opt-in profiler */
 /* Kernel classes: 0 edge-MLP fwd, 1 node-MLP fwd, 2 dense-MLP fwd, 3 edge-MLP bwd-data,

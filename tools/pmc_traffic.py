@@ -18,10 +18,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+HOT_SOURCES = ["mgn_common.h", "mgn_chain.h", "mgn_mlp.hip", "mgn_chain.hip", "mgn_chain16.hip", "mgn_graph.hip"]
+
+
 def sources_sha():
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "graph-physics_amd", "csrc", "*"))) + [
-        os.path.join(ROOT, "include", "mgn.h")]
+    # the training-step kernels only (graph construction in mgn_build.hip does not run in the step)
+    files = [os.path.join(ROOT, "graph-physics_amd", "csrc", f) for f in HOT_SOURCES]
     for f in files:
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
@@ -31,8 +34,10 @@ def kernel_class(name):
     m = re.search(r"mlp_(fwd|bwd)_kernel.*?Li(\d+)ELi(\d+)ELi(\d)E", name)
     if m:
         return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[m.group(4)]
-    for key, cls in (("chain_fwd_kernel", "fwd_edge"), ("chain_bwd_kernel", "bwd_edge"),
-                     ("mlp_wgrad_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
+    for key, cls in (("chain16_node_fwd_kernel", "fwd_node"), ("chain16_node_bwd_kernel", "bwd_node"),
+                     ("chain16_fwd_kernel", "fwd_edge"), ("chain16_bwd_kernel", "bwd_edge"),
+                     ("chain_fwd_kernel", "fwd_edge"), ("chain_bwd_kernel", "bwd_edge"),
+                     ("mlp_wgrad_kernel", "wgrad"), ("wgrad_ring_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
                      ("node_grad_kernel", "combine"), ("node_proj_kernel", "proj"),
                      ("adamw", "adamw"), ("pack_kernel", "pack")):
         if key in name:
