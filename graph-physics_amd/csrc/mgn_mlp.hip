@@ -2212,6 +2212,10 @@ static size_t block_fwd_ws(const mgn_topology* t, const mgn_mlp* edge) {
     return align_up((size_t)t->num_nodes * 2 * edge->hidden * sizeof(float));
 }
 
+int mgn_block_forward_inference_supported(const mgn_mlp* edge, const mgn_mlp* node) {
+    return chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) ? 1 : 0;
+}
+
 size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
     (void)node;
     return block_fwd_ws(t, edge);
@@ -2225,8 +2229,15 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     const int H = edge->hidden;
     MGN_REQUIRE(edge->in_dim == 3 * H && edge->out_dim == H, "edge MLP must be 3h -> h");
     MGN_REQUIRE(node->in_dim == 2 * H && node->out_dim == H && node->hidden == H, "node MLP must be 2h -> h");
-    MGN_REQUIRE(saved->edge.z && saved->edge.rden && saved->aggr, "block saved buffers missing");
+    MGN_REQUIRE(saved->edge.z && saved->edge.rden, "block saved buffers missing");
     MGN_REQUIRE(edge->dtype == node->dtype, "edge/node MLP dtype mismatch");
+    // inference (saved->edge.act == NULL): the chained bf16 h=128 kernels skip every backward save
+    const bool infer = saved->edge.act == nullptr;
+    MGN_REQUIRE(infer || saved->aggr, "block saved buffers missing");
+    MGN_REQUIRE(!infer || (chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) &&
+                           saved->node.act == nullptr),
+                "inference block forward (saved act = NULL) needs the chained bf16 h=128 path "
+                "(mgn_block_forward_inference_supported)");
     MGN_REQUIRE(ws_bytes >= block_fwd_ws(t, edge) && (ws || t->num_nodes == 0), "block forward workspace too small");
     hipStream_t st = (hipStream_t)stream;
     const int dt = edge->dtype;

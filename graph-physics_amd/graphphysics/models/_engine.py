@@ -231,6 +231,14 @@ def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device):
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
 
 
+def _alloc_block_infer(espec, topo, tdt, device):
+    """Inference scratch of mgn_block_forward (act = NULL): the edge MLP's z/rden only."""
+    z = _empty(topo.num_edges * espec.hidden, tdt, device)
+    rden = _empty(topo.num_edges, torch.float32, device)
+    se = nat.MlpSaved(0, 0, z.data_ptr(), rden.data_ptr())
+    return nat.BlockSaved(se, nat.MlpSaved(0, 0, 0, 0), 0), (z, rden)
+
+
 def _permute(src, idx, rows, cols, in_mdt, out_tdt, scatter, stream, out=None):
     if out is None:
         out = torch.empty((rows, cols), dtype=out_tdt, device=src.device)
@@ -312,7 +320,11 @@ class EPDFunction(torch.autograd.Function):
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
             if train or scratch is None:
-                sv = _alloc_block_saved(bdescs[2 * b], bdescs[2 * b + 1], es_, ns_, topo, tdt, dev)
+                if not train and nat.lib().mgn_block_forward_inference_supported(
+                        ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1])):
+                    sv = _alloc_block_infer(es_, topo, tdt, dev)  # no backward saves
+                else:
+                    sv = _alloc_block_saved(bdescs[2 * b], bdescs[2 * b + 1], es_, ns_, topo, tdt, dev)
                 if not train:
                     scratch = sv
             else:
@@ -421,7 +433,12 @@ class BlockFunction(torch.autograd.Function):
         e0 = _permute(edge_attr.detach().contiguous(), topo.csc_eid, E, H,
                       nat.mgn_dtype(edge_attr.dtype) if edge_attr.dtype in (torch.float32, torch.bfloat16)
                       else nat.MGN_F32, tdt, False, st) if E else torch.empty((0, H), dtype=tdt, device=dev)
-        sv = _alloc_block_saved(pw.descs[0], pw.descs[1], espec, nspec, topo, tdt, dev)
+        train = any(ctx.needs_input_grad)
+        if not train and nat.lib().mgn_block_forward_inference_supported(ctypes.byref(pw.descs[0]),
+                                                                         ctypes.byref(pw.descs[1])):
+            sv = _alloc_block_infer(espec, topo, tdt, dev)
+        else:
+            sv = _alloc_block_saved(pw.descs[0], pw.descs[1], espec, nspec, topo, tdt, dev)
         x1 = torch.empty((N, H), dtype=tdt, device=dev)
         e1 = torch.empty((max(E, 1), H), dtype=tdt, device=dev)
         fws = _fwd_ws_block(topo, pw.descs[0], pw.descs[1], dev)
@@ -430,7 +447,7 @@ class BlockFunction(torch.autograd.Function):
             nat.ptr(e0), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), nat.ptr(fws), fws.numel(), st))
         e_out = _permute(e1, topo.csc_eid, E, H, mdt, x.dtype, True, st) if E else \
             torch.empty((0, H), dtype=x.dtype, device=dev)
-        if any(ctx.needs_input_grad):
+        if train:
             ctx.plan, ctx.mdt, ctx.topo, ctx.pw = plan, mdt, topo, pw
             ctx.state = (x0, e0, sv)
             ctx.xdtype = x.dtype

@@ -142,7 +142,13 @@ typedef struct mgn_block_saved {
 /* x:[N,h], e:[E,h] (target-sorted edge order), dtype of the MLPs. x_out/e_out may not alias.
  * The edge MLP's first Linear on [e ‖ x_i ‖ x_j] is evaluated as e·W0aᵀ + P_i[dst] + P_j[src]
  * with the node projections P = [x·W0bᵀ ‖ x·W0cᵀ] (fp32, N rows) computed once per block into
- * ws (scratch, free again when the call's work has run). */
+ * ws (scratch, free again when the call's work has run).
+ * Inference (no autograd, e.g. the reference's validation/rollout _make_prediction under
+ * torch.no_grad, lightning_module.py:168-202): saved->edge.act = saved->node.act = NULL selects
+ * kernels that write only the edge MLP's z/rden (scratch the node MLP's aggregation reads) and no
+ * backward saves; aggr and the node saves may be NULL. Available where
+ * mgn_block_forward_inference_supported() is 1 (bf16, h = 128, 4 layers + RMSNorm). */
+int mgn_block_forward_inference_supported(const mgn_mlp* edge, const mgn_mlp* node);
 size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
                                          const mgn_mlp* node);
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,

@@ -167,7 +167,8 @@ def test_k_hop_graph_and_preprocessing_pipeline():
     kei = GO.k_hop_edge_index(ei, 2, n)
     assert torch.equal(kg.edge_index.cpu(), kei)
     torch.testing.assert_close(kg.edge_attr.cpu(), GO.edge_features(pos, kei), rtol=2.5e-7, atol=1e-12)
-    # default world-pos block (x[:, 0:3]) appended: 3 + 1 + 3 + 1 columns (torch_graph.py:101-110)
-    kg8 = compute_k_hop_graph(g, 2, add_edge_features_to_khop=True)
-    assert kg8.edge_attr.shape == (kei.shape[1], 8)
-    torch.testing.assert_close(kg8.edge_attr[:, 4:].cpu(), GO.edge_features(x, kei), rtol=2.5e-7, atol=1e-12)
+    # default world-pos block (x[:, 0:3]) appended (torch_graph.py:101-110): 2D Cartesian + Distance
+    # (3 columns) then 3D relative world pos + norm (4 columns)
+    kg7 = compute_k_hop_graph(g, 2, add_edge_features_to_khop=True)
+    assert kg7.edge_attr.shape == (kei.shape[1], 7)
+    torch.testing.assert_close(kg7.edge_attr[:, 3:].cpu(), GO.edge_features(x, kei), rtol=2.5e-7, atol=1e-12)

@@ -1,0 +1,139 @@
+"""Validation rollout (reference lightning_module.py:17-25,163-249) and the inference block kernels.
+
+Tolerances: fp32 rollout vs the CPU oracle rollout (same weights, same normaliser statistics,
+reference _make_prediction loop restated below): per-step predictions max|Δ| ≤ 1e-4·(1+|ref|),
+rollout RMSE and per-step val losses within 1e-6 relative-ish (|Δ| ≤ 1e-6 + 1e-4·ref). Graph-replayed
+rollout ≡ eager rollout bit for bit (same kernels, same order). bf16 h=128: the inference kernels
+(no backward saves) produce bit-identical outputs to the training-mode kernels.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    import __graft_entry__ as ge
+
+    ge.build()
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+def _sim(dtype, mp, h):
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=dtype)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, m, DEV)
+    # normaliser statistics from two training-mode forwards
+    for t in (0, 1):
+        b = meshes.cylinder_batch(2, t=t, jitter=0.01)
+        with torch.no_grad():
+            sim(Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")}))
+    sim.eval()
+    return sim
+
+
+def _frames(nsteps=5):
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    out = []
+    for t in range(nsteps):
+        b = meshes.cylinder_batch(1, t=t)
+        out.append({k: torch.from_numpy(b[k]) for k in ("x", "y", "edge_index", "edge_attr")})
+    return out, Data
+
+
+def _oracle_rollout(sim, frames, mp, h):
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    ref.load_state_dict({k: v.detach().float().cpu() for k, v in sim.model.state_dict().items()})
+    osim = O.OracleSimulator(ref, 11, 3, 2)
+    for mine, theirs in ((sim._output_normalizer, osim.out_norm), (sim._node_normalizer, osim.node_norm),
+                         (sim._edge_normalizer, osim.edge_norm)):
+        theirs.acc_sum, theirs.acc_sum_squared = mine._acc_sum.cpu(), mine._acc_sum_squared.cpu()
+        theirs.acc_count, theirs.num_acc = mine._acc_count.cpu(), mine._num_accumulations.cpu()
+    last, preds, losses = None, [], []
+    for f in frames:  # lightning_module.py:168-202 with the batch cloned
+        x, y = f["x"].clone(), f["y"]
+        if last is not None:
+            x[:, 0:2] = last
+        nt = x[:, 2]
+        mask = ~((nt == 0) | (nt == 5))
+        with torch.no_grad():
+            _, _, pred = osim.forward(x, y, f["edge_index"], f["edge_attr"], training=False)
+        pred[mask] = y[mask]
+        last = pred
+        preds.append(pred)
+        losses.append(O.l2_loss(y, pred, nt).item())
+    p, t = torch.cat(preds), torch.cat([f["y"] for f in frames])
+    return torch.stack(preds), losses, float(torch.sqrt(((p - t) ** 2).mean()))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rollout_fp32_vs_oracle(graph):
+    from graphphysics.training.rollout import Rollout
+
+    mp, h = 5, 32
+    sim = _sim(torch.float32, mp, h)
+    frames, Data = _frames()
+    ref, ref_losses, ref_rmse = _oracle_rollout(sim, frames, mp, h)
+    ro = Rollout(sim, node_type_index=2, graph=graph)
+    got = ro.rollout([Data(**{k: v.to(DEV) for k, v in f.items()}) for f in frames]).cpu()
+    tol = 1e-4 * (1 + ref.abs())
+    assert bool(((got - ref).abs() <= tol).all()), float((got - ref).abs().max())
+    for a, b in zip([l.item() for l in ro.losses], ref_losses):
+        assert abs(a - b) <= 1e-6 + 1e-4 * b
+    assert abs(ro.all_rollout_rmse() - ref_rmse) <= 1e-6 + 1e-4 * ref_rmse
+
+
+def test_rollout_graph_equals_eager_bf16_h128():
+    from graphphysics.training.rollout import Rollout
+
+    sim = _sim(torch.bfloat16, 15, 128)
+    frames, Data = _frames()
+    dev_frames = [Data(**{k: v.to(DEV) for k, v in f.items()}) for f in frames]
+    a = Rollout(sim, 2, graph=False).rollout(dev_frames)
+    b = Rollout(sim, 2, graph=True).rollout(dev_frames)
+    assert torch.equal(a, b)
+    # trajectory changes mesh: new edge_index tensor → re-recorded graph, still equal to eager
+    from graphphysics.utils import meshes
+
+    bb = meshes.cylinder_batch(2, t=0, jitter=0.01)
+    two = [Data(**{k: torch.from_numpy(bb[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})] * 3
+    ro = Rollout(sim, 2, graph=True)
+    ro.rollout(dev_frames)
+    assert torch.equal(ro.rollout(two), Rollout(sim, 2, graph=False).rollout(two))
+
+
+def test_inference_block_kernels_match_training_kernels():
+    """bf16 h=128: mgn_block_forward with act = NULL (no backward saves) is bit-identical to the
+    training-mode forward (same arithmetic, fewer stores)."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(8, jitter=0.01)
+    g = Data(x=torch.randn(b["x"].shape[0], 11, device=DEV), edge_index=torch.from_numpy(b["edge_index"]).to(DEV),
+             edge_attr=torch.from_numpy(b["edge_attr"]).to(DEV))
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(15, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
+    y_train = m(g)  # parameters require grad: training kernels with saves
+    assert y_train.requires_grad
+    with torch.no_grad():
+        y_inf = m(g)
+    assert torch.equal(y_train.detach(), y_inf)
+    from graphphysics import _native as nat
+
+    d = m._get_plan().packed(DEV, nat.MGN_BF16).descs
+    import ctypes
+
+    assert nat.lib().mgn_block_forward_inference_supported(ctypes.byref(d[3]), ctypes.byref(d[4])) == 1
