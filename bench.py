@@ -50,7 +50,47 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel step (exchanges + split graph) even on one rank")
+    ap.add_argument("--workload", default="cylinder", choices=["cylinder", "aneurysm"],
+                    help="cylinder: Cfg B (headline); aneurysm: Cfg E (1 k-hop-2 aneurysm graph per GPU)")
     return ap.parse_args()
+
+
+def make_workload(a, dev, rank, mesh):
+    """Host arrays + device Data + Simulator layout of the benchmarked configuration.
+    cylinder (Cfg B, BASELINE.json configs[1]): a.batch jittered copies of the CylinderFlow mesh.
+    aneurysm (Cfg E, configs[4] per GPU): the reference's 3D aneurysm mock mesh (N=22,535,
+    115,275 tetrahedra), graph built ON DEVICE by libmgn (FaceToEdge → k-hop 2 → Cartesian +
+    Distance: E=1,395,256, max in-degree 103), synthetic node features (14 channels + node type),
+    Simulator layout of coarse-aneurysm.json (features 0:14, outputs 0:3, type at 14)."""
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    if a.workload == "cylinder":
+        b = meshes.cylinder_batch(a.batch, t=0, jitter=0.01, seed=1234 + rank, mesh=mesh)
+        data = Data(x=torch.from_numpy(b["x"]).to(dev), y=torch.from_numpy(b["y"]).to(dev),
+                    edge_index=torch.from_numpy(b["edge_index"]).to(dev),
+                    edge_attr=torch.from_numpy(b["edge_attr"]).to(dev), pos=torch.from_numpy(b["pos"]).to(dev))
+        return b, data, dict(node_in=11, edge_in=3, out=2, fs=(0, 2), os=(0, 2), nti=2), \
+            "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, a.hidden, a.batch), \
+            "%d jittered copies of the reference in-tree CylinderFlow mesh per GPU" % a.batch
+    from graphphysics.utils import graph_build as G
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "aneurysm_mesh.npz"))
+    pos = torch.from_numpy(z["pos"]).to(dev)
+    tet = torch.from_numpy(z["tetra"].astype(np.int64)).t().contiguous().to(dev)
+    n = pos.shape[0]
+    ei = G.k_hop_edge_index(G.face_to_edge(tet, n), 2, n)
+    ea = G.edge_features(pos, ei)
+    rng = np.random.default_rng(1234 + rank)
+    feats = rng.standard_normal((n, 14)).astype(np.float32)
+    nt = rng.choice([0, 4, 5, 6], size=n, p=[0.9, 0.01, 0.01, 0.08]).astype(np.float32)
+    x = np.concatenate([feats, nt[:, None]], 1)
+    y = (feats[:, 0:3] + 0.01 * rng.standard_normal((n, 3))).astype(np.float32)
+    data = Data(x=torch.from_numpy(x).to(dev), y=torch.from_numpy(y).to(dev), edge_index=ei, edge_attr=ea, pos=pos)
+    b = {"x": x, "y": y, "edge_index": ei.cpu().numpy(), "edge_attr": ea.cpu().numpy()}
+    return b, data, dict(node_in=23, edge_in=4, out=3, fs=(0, 14), os=(0, 3), nti=14), \
+        "3D-CoarseAneurysm MGN %dMP h=%d, 1 graph per GPU, k-hop 2 (Cfg E)" % (a.mp, a.hidden), \
+        "reference aneurysm mock mesh (k-hop 2 built on device), synthetic node features"
 
 
 def flops_per_block(n, e, h):
@@ -108,14 +148,12 @@ def main():
     nat.load()
     cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     mesh = meshes.load_cylinder_mesh()
-    b = meshes.cylinder_batch(a.batch, t=0, jitter=0.01, seed=1234 + rank, mesh=mesh)
-    data = Data(x=torch.from_numpy(b["x"]).to(dev), y=torch.from_numpy(b["y"]).to(dev),
-                edge_index=torch.from_numpy(b["edge_index"]).to(dev),
-                edge_attr=torch.from_numpy(b["edge_attr"]).to(dev), pos=torch.from_numpy(b["pos"]).to(dev))
+    b, data, lay, workload, datadesc = make_workload(a, dev, rank, mesh)
     N, E = data.x.shape[0], data.edge_index.shape[1]
     torch.manual_seed(0)
-    model = EncodeProcessDecode(a.mp, 2 + NodeType.SIZE, 3, 2, a.hidden, compute_dtype=cdt)
-    sim = Simulator(2 + NodeType.SIZE, 3, 2, 0, 2, 0, 2, 2, model, dev)
+    model = EncodeProcessDecode(a.mp, lay["node_in"], lay["edge_in"], lay["out"], a.hidden, compute_dtype=cdt)
+    sim = Simulator(lay["node_in"], lay["edge_in"], lay["out"], lay["fs"][0], lay["fs"][1], lay["os"][0],
+                    lay["os"][1], lay["nti"], model, dev)
     params = list(sim.parameters())
     opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
     sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
@@ -181,8 +219,8 @@ def main():
         roof = {"kernel": dom, "bound": bound, **(hbm if bound == "hbm" else mfma), "traffic": None,
                 "bytes_per_launch": alg_bytes[dom], "flops_per_launch": alg_flops[dom],
                 "avg_launch_us": round(avg_s * 1e6, 2), "hbm": hbm, "mfma": mfma}
-        step_flops = 3 * (a.mp * (fe + fn) + 2 * (3 * h + 3 * h * h) * E + 2 * (11 * h + 3 * h * h) * N
-                          + 2 * (3 * h * h + h * 2) * N)
+        step_flops = 3 * (a.mp * (fe + fn) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
+                          + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
         roof["step_tflops_per_s"] = round(step_flops * a.steps / dt / 1e12, 2)
     if roof is not None:
         roof["traffic"], roof["traffic_note"] = pmc_traffic(roof["kernel"])
@@ -191,21 +229,21 @@ def main():
         "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-        "data": "synthetic: %d jittered copies of the reference in-tree CylinderFlow mesh per GPU, "
-                "random-init weights (seed 0)" % a.batch,
+        "data": "synthetic: %s, random-init weights (seed 0)" % datadesc,
         "execution": ("eager" if not step.use_graph else
                       "hipGraph replay of forward+loss+backward; eager statistics/gradient all-reduce + AdamW"
                       if step.dp else "hipGraph replay of the whole step"),
-        "config": {"workload": "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, h, a.batch),
-                   "nodes_per_gpu": N, "edges_per_gpu": E, "global_batch": a.batch * world,
-                   "parallelism": "dp%d" % world, "graphs_per_sec": round(value * a.batch, 2)},
+        "config": {"workload": workload, "nodes_per_gpu": N, "edges_per_gpu": E,
+                   "global_batch": (a.batch if a.workload == "cylinder" else 1) * world,
+                   "parallelism": "dp%d" % world,
+                   "graphs_per_sec": round(value * (a.batch if a.workload == "cylinder" else 1), 2)},
         "roofline": roof, "kernels": kinds, "last_loss": last_loss,
     }
 
-    if not a.no_mse:
+    if not a.no_mse and a.workload == "cylinder":
         out["one_step_mse"] = one_step_mse(sim, mesh, dev, a)
     if world == 1 and a.cpu_steps > 0:
-        out["cpu_baseline"] = cpu_baseline(a, b, mesh)
+        out["cpu_baseline"] = cpu_baseline(a, b, lay)
         if out["cpu_baseline"]:
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
     print(json.dumps(out), flush=True)
@@ -270,7 +308,7 @@ def one_step_mse(sim, mesh, dev, a):
             "frames": "3->4, 4->5 (held out), B=1, weights after the timed steps"}
 
 
-def cpu_baseline(a, b, mesh):
+def cpu_baseline(a, b, lay):
     """The reference algorithm on the host (oracle = op-for-op restatement of the reference's
     PyTorch CPU path, pinned to golden vectors), same workload (Cfg B batch 8), fp32, all cores."""
     from oracle import mgn_oracle as O
@@ -279,8 +317,9 @@ def cpu_baseline(a, b, mesh):
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     torch.set_num_threads(cores)
     torch.manual_seed(0)
-    ref = O.OracleEPD(a.mp, 11, 3, 2, a.hidden)
-    osim = O.OracleSimulator(ref, 11, 3, 2)
+    ref = O.OracleEPD(a.mp, lay["node_in"], lay["edge_in"], lay["out"], a.hidden)
+    osim = O.OracleSimulator(ref, lay["node_in"], lay["edge_in"], lay["out"], feature_slice=lay["fs"],
+                             output_slice=lay["os"], node_type_index=lay["nti"])
     opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
     x, y = torch.from_numpy(b["x"]), torch.from_numpy(b["y"])
     ei, ea = torch.from_numpy(b["edge_index"]), torch.from_numpy(b["edge_attr"])
@@ -288,7 +327,7 @@ def cpu_baseline(a, b, mesh):
     def step():
         opt.zero_grad()
         net, tdn, _ = osim.forward(x, y, ei, ea, True)
-        O.l2_loss(tdn, net, x[:, 2]).backward()
+        O.l2_loss(tdn, net, x[:, lay["nti"]]).backward()
         opt.step()
 
     step()  # warm-up
@@ -310,7 +349,7 @@ def cpu_baseline(a, b, mesh):
     except OSError:
         pass
     return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": cores, "kind": "port",
-            "sample": "%d timed + 1 warm-up full Cfg B steps (batch 8, N=%d, E=%d), torch %s fp32, median"
+            "sample": "%d timed + 1 warm-up full steps of the same workload (N=%d, E=%d), torch %s fp32, median"
                       % (a.cpu_steps, b["x"].shape[0], b["edge_index"].shape[1], torch.__version__),
             "cpu": model, "host": platform.node()}
 
