@@ -12,10 +12,15 @@
 // is the accumulator with no data movement, given weights staged in that permuted k order.
 // ReLU masks: 32 bits per lane (bit 4t + r) per tile and layer; the backward has the same map.
 #include <cmath>
+#include <utility>
 #include <cstring>
 #include <mutex>
 
 #include "mgn_chain.h"
+
+#ifndef MGN_NODE_AG
+#define MGN_NODE_AG 8  // in-edges gathered per round trip by the node-MLP aggregation
+#endif
 
 namespace {
 
@@ -100,13 +105,30 @@ __device__ __forceinline__ unsigned push_bit(unsigned w, float v) {
 }
 __device__ __forceinline__ int bit_sel(unsigned w, int k) { return (int)(w << k) >> 31; }
 
+// acc (tile layout, element 4t + r) &= sign-extended bit 31 - (4t + r) of w: one v_bfe_i32 + v_and
+// per element (left to the compiler, the select becomes v_cmp + v_cndmask with SGPR-hazard s_nops)
+template <int K>
+__device__ __forceinline__ int bfe_sel(unsigned w) {
+    int r;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(w), "n"(31 - K));
+    return r;
+}
+template <int... K>
+__device__ __forceinline__ void relu_mask_seq(f4 (&acc)[8], unsigned w, std::integer_sequence<int, K...>) {
+    ((acc[K >> 2][K & 3] = __int_as_float(__float_as_int(acc[K >> 2][K & 3]) & bfe_sel<K>(w))), ...);
+}
+__device__ __forceinline__ void relu_mask(f4 (&acc)[8], unsigned w) {
+    relu_mask_seq(acc, w, std::make_integer_sequence<int, 32>{});
+}
+
 // Weight image: fragment (l, t, s) lane (r, g) element j = A_l[16t + r][32s + 16(j>>2) + 4g + (j&3)]
 // (A = W forward, Wᵀ backward). Linear walk over libmgn's 16x16x32 packs (16-byte coalesced loads):
 // a source chunk holds 8 consecutive reduction indices 32s + 8q .. +7 of one row; its halves go to
 // lane groups g = 2(q&1) + half, element group jg = q>>1.
+template <int NL = 4>
 __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
                                         bool transposed) {
-    constexpr int PER = 4 * 2048 / (NW * 64);  // 16 chunks per thread
+    constexpr int PER = NL * 2048 / (NW * 64);  // 16 chunks per thread (4 layers)
     u32x4 v[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -538,6 +560,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         const float rq = __builtin_amdgcn_rcpf(qd);
         const float rms = qd - RMS_EPS;
         const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
+        // rows past the end (last tile) are zeroed by a bit mask: a select on `ok` compiles to one
+        // exec-masked branch per element (8x the VALU work of this phase)
+        const int okm = ok ? -1 : 0;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 z = bf4(nxt.z[t]);
@@ -546,8 +571,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float dy = acc[t][r];
-                acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
-                ds[r] = ok ? dy * z[r] * rq : 0.f;
+                acc[t][r] = __int_as_float(__float_as_int(fmaf(-z[r], coef, sc[r] * dy * rq)) & okm);
+                ds[r] = __int_as_float(__float_as_int(dy * z[r] * rq) & okm);
             }
             const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
             if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
@@ -573,12 +598,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             // stores its B operand dZ_l (R8) under the MFMAs
             gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
             STAMP(3);
-            const unsigned bw = mcur[l - 1];
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    acc[t][r] = __int_as_float(__float_as_int(acc[t][r]) & bit_sel(bw, 4 * t + r));
+            relu_mask(acc, mcur[l - 1]);
             to_operand(acc, B);
             STAMP(4);
         }
@@ -609,11 +629,20 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 // ------------------------------------------------------------------------------------ node MLP
 // A-operand fragment (chain k order) read from a 16x16x32 pack in global memory (L2-resident):
 // source tile `tile` (relative to the layer base); two 8-byte pieces per lane.
-__device__ __forceinline__ bf16x8 gfrag(const __bf16* pack, int64_t tile, int lane) {
+// Buffer loads: the lane part of the address is one 32-bit VGPR (gfrag_voff) and the tile part a
+// scalar offset, so the compiler cannot hoist 64 per-fragment 64-bit addresses out of the tile
+// loop (with global loads it did, and the node kernels spilled).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gfrag_rsrc(const __bf16* pack) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(pack), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ int gfrag_voff(int lane) {
     const int r = lane & 15, g = lane >> 4;
-    const __bf16* p = pack + (tile * 64 + r) * 8 + 4 * (g & 1);
-    const u32x2 lo = *reinterpret_cast<const u32x2*>(p + 16 * (g >> 1) * 8);
-    const u32x2 hi = *reinterpret_cast<const u32x2*>(p + 16 * (2 + (g >> 1)) * 8);
+    return (r * 8 + 4 * (g & 1) + 16 * (g >> 1) * 8) * 2;  // bytes
+}
+__device__ __forceinline__ bf16x8 gfrag(__amdgpu_buffer_rsrc_t rs, int voff, int tile) {
+    const int so = tile * 64 * 8 * 2;  // bytes
+    const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so, 0));
+    const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so + 2 * 16 * 8 * 2, 0));
     const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
     return __builtin_bit_cast(bf16x8, w);
 }
@@ -623,16 +652,18 @@ __device__ __forceinline__ bf16x8 gfrag(const __bf16* pack, int64_t tile, int la
 template <class TileFn>
 __device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, const bf16x8 (&Bx)[4],
                                               const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
+    const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(pack);
+    const int vo = gfrag_voff(lane);
     gemm16(acc, W, 0, Bx, lane);
     bf16x8 fr[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) fr[t] = gfrag(pack, tile_of(t, 0), lane);
+    for (int t = 0; t < 8; ++t) fr[t] = gfrag(rs, vo, tile_of(t, 0));
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         bf16x8 nf[8];
         if (s + 1 < 4) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) nf[t] = gfrag(pack, tile_of(t, s + 1), lane);
+            for (int t = 0; t < 8; ++t) nf[t] = gfrag(rs, vo, tile_of(t, s + 1));
         }
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], Ba[s], acc[t]);
@@ -652,19 +683,32 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
     const int m = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
+    // the first tile's segment bounds load under the weight staging (most waves own at most one
+    // node tile: its chain of dependent loads is most of the kernel's time)
+    int kb = 0, ke = 0;
+    auto load_seg = [&](int64_t tl) {
+        const int64_t row = tl * TR + m;
+        const int64_t v = clamp_row(row, a.M);
+        kb = a.seg_ptr[v];
+        ke = row < a.M ? a.seg_ptr[v + 1] : kb;
+    };
+    if (tile < a.ntiles) load_seg(tile);
     stage16(W, a.wpack, a.woff, a.wks, false);
     for (int i = threadIdx.x; i < 6 * H; i += NW * 64)
         vec[i] = i < 4 * H ? a.bias[i / H][i % H] : i < 5 * H ? a.scale[i - 4 * H] : a.agg_scale[i - 5 * H];
+    STAMP_DECL;
     __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * NW;
-    for (int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x; tile < a.ntiles; tile += stride) {
+    STAMP(0);
+    for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
+        if (tile != first) load_seg(tile);
         const int64_t row = tile * TR + m;
         const bool ok = row < a.M;
-        const int64_t v = clamp_row(row, a.M);
         // x rows (layer-0 B operand of the x block, and the residual)
         bf16x8 xb[4];
         {
-            const __bf16* xp = a.x + v * H + 4 * g;
+            const __bf16* xp = a.x + clamp_row(row, a.M) * H + 4 * g;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const u32x2 lo = *reinterpret_cast<const u32x2*>(xp + 32 * s);
@@ -674,34 +718,37 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
             }
         }
         // aggregation over the node's in-edges (target-sorted: one contiguous segment), in the
-        // accumulator layout: the lane sums its 32 features of every message s_e ⊙ z_k / q_k
+        // accumulator layout: the lane sums its 32 features of every message s_e ⊙ z_k / q_k, in
+        // edge order. Groups of AG edges: every load of a group is issued before the first add
+        // (one memory round trip per group; edges past the segment end reload its last edge and
+        // add 0 · z)
+        constexpr int AG = MGN_NODE_AG;
         f4 agg[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) agg[t] = f4{0.f, 0.f, 0.f, 0.f};
-        {
-            int k = a.seg_ptr[v];
-            const int ke = ok ? a.seg_ptr[v + 1] : k;
-            for (; k < ke; k += 2) {
-                const bool two = k + 1 < ke;
-                const int k1 = two ? k + 1 : k;
-                u32x2 z0[8], z1[8];
-                const __bf16* zp0 = a.agg_z + (int64_t)k * H + 4 * g;
-                const __bf16* zp1 = a.agg_z + (int64_t)k1 * H + 4 * g;
+#pragma unroll 1
+        for (int k = kb; k < ke; k += AG) {
+            u32x2 zz[AG][8];
+            float rr[AG];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    z0[t] = *reinterpret_cast<const u32x2*>(zp0 + 16 * t);
-                    z1[t] = *reinterpret_cast<const u32x2*>(zp1 + 16 * t);
-                }
-                const float r0 = __builtin_amdgcn_rcpf(a.agg_rden[k]);
-                const float r1 = two ? __builtin_amdgcn_rcpf(a.agg_rden[k1]) : 0.f;
+            for (int u = 0; u < AG; ++u) {
+                const int ku = k + u < ke ? k + u : ke - 1;
+                const __bf16* zp = a.agg_z + (int64_t)ku * H + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) zz[u][t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
+                rr[u] = a.agg_rden[ku];
+            }
+#pragma unroll
+            for (int u = 0; u < AG; ++u) {
+                const float r = k + u < ke ? __builtin_amdgcn_rcpf(rr[u]) : 0.f;
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     const f4 sc = *reinterpret_cast<const f4*>(vec + 5 * H + 16 * t + 4 * g);
-                    agg[t] += sc * (bf4(z0[t]) * r0);
-                    agg[t] += sc * (bf4(z1[t]) * r1);
+                    agg[t] += sc * (bf4(zz[u][t]) * r);
                 }
             }
         }
+        STAMP(1);
         if (SAVE) store_rows(agg, scr, a.aggr_save, tile, a.M, lane);
         bf16x8 Ba[4];
         to_operand(agg, Ba);
@@ -711,7 +758,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         for (int l = 0; l < 3; ++l) {
             if (l == 0)
                 gemm16_layer0(acc, W, xb, Ba, a.wpack + a.woff[0],
-                              [](int t, int s) { return (int64_t)(t * 8 + 4 + s); }, lane);
+                              [](int t, int s) { return t * 8 + 4 + s; }, lane);
             else
                 gemm16(acc, W, l, B, lane);
             unsigned bits = 0u;
@@ -732,6 +779,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
             }
         }
         gemm16(acc, W, 3, B, lane);
+        STAMP(2);
         float ss = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -759,7 +807,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                 acc[t][r] = fmaf(sc[r], acc[t][r] * rq, (float)xb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
+        STAMP(3);
     }
+    STAMP_PRINT("nfwd16");
 }
 
 __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdArgs a) {
@@ -774,7 +824,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     stage16(W, a.wtpack, a.woff, a.wks, true);
     for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
     for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
+    STAMP_DECL;
     __syncthreads();
+    STAMP(0);
     const int64_t stride = (int64_t)gridDim.x * NW;
     for (int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x; tile < a.ntiles; tile += stride) {
         const int64_t row = tile * TR + m;
@@ -809,6 +861,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         const float rq = __builtin_amdgcn_rcpf(qd);
         const float rms = qd - RMS_EPS;
         const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
+        const int okm = ok ? -1 : 0;  // bit mask, not a select (see chain16_bwd_kernel)
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 z = bf4(zr[t]);
@@ -817,23 +870,20 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float dy = acc[t][r];
-                acc[t][r] = ok ? fmaf(-z[r], coef, sc[r] * dy * rq) : 0.f;
-                ds[r] = ok ? dy * z[r] * rq : 0.f;
+                acc[t][r] = __int_as_float(__float_as_int(fmaf(-z[r], coef, sc[r] * dy * rq)) & okm);
+                ds[r] = __int_as_float(__float_as_int(dy * z[r] * rq) & okm);
             }
             const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
             if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
         }
+        STAMP(1);
         bf16x8 B[4];
         to_operand(acc, B);
         store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
 #pragma unroll
         for (int l = 3; l >= 1; --l) {
             gemm16(acc, W, l, B, lane);
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    acc[t][r] = __int_as_float(__float_as_int(acc[t][r]) & bit_sel(mk[l - 1], 4 * t + r));
+            relu_mask(acc, mk[l - 1]);
             to_operand(acc, B);
             store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
         }
@@ -843,20 +893,23 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
         store_rows(acc, scr, a.dx_part, tile, a.M, lane);
         {
-            const __bf16* pk = a.wtpack + a.woff[0];
+            const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
+            const int vo = gfrag_voff(lane);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 bf16x8 fr[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) fr[t] = gfrag(pk, (int64_t)((8 + t) * 4 + s), lane);
+                for (int t = 0; t < 8; ++t) fr[t] = gfrag(rs, vo, (8 + t) * 4 + s);
 #pragma unroll
                 for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], B[s], acc[t]);
             }
         }
         store_rows(acc, scr, a.d_aggr, tile, a.M, lane);
+        STAMP(2);
     }
+    STAMP_PRINT("nbwd16");
     __syncthreads();
     if (threadIdx.x < H) {
         float s2 = 0.f;
