@@ -122,12 +122,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != a.gpus:
         a.gpus = world
+    # MGN_DIST_BACKEND=gloo (rehearsal only): several ranks share the visible GPUs round-robin and
+    # exchange through host memory; the default "nccl" is RCCL over xGMI, one rank per GPU
+    backend = os.environ.get("MGN_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or a.dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)  # RCCL over xGMI
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     import __graft_entry__ as ge
 
     if rank == 0:
