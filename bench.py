@@ -106,8 +106,8 @@ def bytes_per_block(n, e, h, es):
     mask = 3 * h // 8  # ReLU bits of the 3 hidden layers
     edge_fwd = e * (es * h + es * h * 2 + 3 * es * h + mask + 4 + 2 * 4 * h)
     # e in | out, z | R8 inputs of layers 1..3 | masks | rden | fp32 node projections P_i, P_j gathered
-    edge_bwd = e * (3 * es * h + 4 + mask + 4 * es * h + 2 * es * h)
-    # de_out, d_aggr[dst], z in | rden | masks | dZ of 4 layers (R8) | de, dZ0 row-major out
+    edge_bwd = e * (3 * es * h + 4 + mask + 3 * es * h + 2 * es * h)
+    # de_out, d_aggr[dst], z in | rden | masks | dZ of layers 1..3 (R8) | de, dZ0 row-major out
     node_fwd = e * (es * h + 4) + n * (es * h + 3 * es * h + 4 + mask + 3 * es * h)
     # edge z + rden (segment sum) | x in; x_out, aggr, z out; rden; masks; R8 inputs of layers 1..3
     node_bwd = n * (es * h + es * h + 4 + mask + 4 * es * h + 2 * es * h)

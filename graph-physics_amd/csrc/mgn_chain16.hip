@@ -602,8 +602,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             to_operand(acc, B);
             STAMP(4);
         }
-        // layer 0, e block: de = de_out + dZ0 · W0a (stores dZ0 as R8 and row-major under the MFMAs)
-        gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, a.dz0}, tile, a.M);
+        // layer 0, e block: de = de_out + dZ0 · W0a (stores dZ0 row-major under the MFMAs, every
+        // padded row too: the weight-gradient ring reads it as its dZ operand, node_grad as rows)
+        gemm16_st(acc, W, 0, B, lane, scr, StoreDst{nullptr, a.dz0}, tile, a.RP);
         STAMP(6);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] += bf4(dre[t]);

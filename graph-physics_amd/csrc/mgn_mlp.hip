@@ -1081,14 +1081,14 @@ constexpr size_t RG_LDS = (size_t)RG_NS * RG_SLOT;
 // A ring job is self-contained (its own dZ block, X source, row space, chunking and slab target),
 // so one launch can cover several MLPs: WG b runs job j with wg0_j <= b < wg0_j + nchunks_j.
 struct RgJob {
-    const void* z;      // dZ: R8 [RP][128] block of this layer
+    const void* z;      // dZ: R8 [RP][128] block of this layer, or (zrm) row-major [RP][128] rows
     const void* x;      // X: R8 matrix (ld == 0, kp columns) or row-major rows (ld = row stride), both
                         // already offset to this job's first column
     int64_t ld, RP, M;
     float* part;        // slab base of the job's MLP; slab c at part + c * G
     int64_t G, w_off, b_off;
     int32_t n, k, kp, col0;
-    int32_t rows_per_chunk, nchunks, wg0, pad;
+    int32_t rows_per_chunk, nchunks, wg0, zrm;  // zrm: dZ row-major (needs a row-major X: ld != 0)
 };
 struct RgArgs {
     int32_t njobs, pad;
@@ -1121,11 +1121,13 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
     const __bf16* X = reinterpret_cast<const __bf16*>(job.x);
     // this lane's piece of a gathered stage: row 4w + (lane>>4), source chunk for its LDS slot
     const int gr = 4 * w + (lane >> 4), gch = (lane & 15) ^ rg_swz(gr);
+    const bool zrm = job.zrm != 0;
     auto issue = [&](int s) {
         const int sc = s < nst ? s : nst - 1;  // past the end: reload the last stage, never consumed
         const int64_t m0 = r_begin + (int64_t)sc * RG_RS;
         char* slot = smem + (s % RG_NS) * RG_SLOT;
-        glds16(Z + m0 * H + w * 512 + lane * 8, slot + w * 1024);
+        // row-major dZ (rows < RP all written, padding rows zero): the X row image's swizzle
+        glds16(zrm ? Z + (m0 + gr) * H + gch * 8 : Z + m0 * H + w * 512 + lane * 8, slot + w * 1024);
         const __bf16* xs;
         if (!staged) {
             xs = X + (((m0 >> 3) + (w >> 1)) * job.kp + (w & 1) * 64 + lane) * 8;
@@ -1153,10 +1155,49 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
         const char* zi = smem + (s % RG_NS) * RG_SLOT;
         const char* xi = zi + RG_SLOT / 2;
         bf16x8 fa[2], fb[4];
+        if (!zrm) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            fa[i] = *reinterpret_cast<const bf16x8*>(zi + ((lane >> 4) * H + (2 * wn + i) * 16 + (lane & 15)) * 16);
-        if (!staged) {
+            for (int i = 0; i < 2; ++i)
+                fa[i] = *reinterpret_cast<const bf16x8*>(zi + ((lane >> 4) * H + (2 * wn + i) * 16 + (lane & 15)) * 16);
+        }
+        if (zrm) {
+            // dZ and X both row images: A fragments of feature blocks 2wn+i and B fragments of
+            // column blocks 4wk+j by the same transposed reads (A[n][m] = dZ[m][n] has the form
+            // of B[m][n'] = X[m][n'])
+            const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+            const int r0 = 8 * (lane >> 4) + q;
+            const unsigned zb = (unsigned)(uintptr_t)(zi), xb = (unsigned)(uintptr_t)(xi);
+            u32x2 zl[2], zh[2], lo[4], hi[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int ch = (2 * wn + i) * 2 + (p >> 1);
+                const unsigned a0 = zb + r0 * (H * 2) + 16 * (ch ^ rg_swz(r0)) + 8 * (p & 1);
+                const unsigned a1 = zb + (r0 + 4) * (H * 2) + 16 * (ch ^ rg_swz(r0 + 4)) + 8 * (p & 1);
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(zl[i]) : "v"(a0));
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(zh[i]) : "v"(a1));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = (4 * wk + j) * 2 + (p >> 1);
+                const unsigned a0 = xb + r0 * (H * 2) + 16 * (ch ^ rg_swz(r0)) + 8 * (p & 1);
+                const unsigned a1 = xb + (r0 + 4) * (H * 2) + 16 * (ch ^ rg_swz(r0 + 4)) + 8 * (p & 1);
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[j]) : "v"(a0));
+                asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi[j]) : "v"(a1));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(zl[0]), "+v"(zl[1]), "+v"(zh[0]), "+v"(zh[1]), "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]),
+                           "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]));
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const u32x4 v = {zl[i][0], zl[i][1], zh[i][0], zh[i][1]};
+                fa[i] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32x4 v = {lo[j][0], lo[j][1], hi[j][0], hi[j][1]};
+                fb[j] = __builtin_bit_cast(bf16x8, v);
+            }
+        } else if (!staged) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 fb[j] = *reinterpret_cast<const bf16x8*>(xi + ((lane >> 4) * H + (4 * wk + j) * 16 + (lane & 15)) * 16);
@@ -1738,7 +1779,7 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BlockWgradIn {
     int64_t E, N;
     const void *e, *x, *aggr;
-    const void *eact, *edz8, *dP8;
+    const void *eact, *edz8, *dz0, *dP8;  // dz0: row-major [RP][H] dZ of the edge layer 0
     const float* edsp;
     int entiles;
     float *epart, *egrads;
@@ -1808,9 +1849,10 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
         int n, k;
         mlp_layer_shape(*edge, l, &n, &k);
         const __bf16* z = edz + (int64_t)l * RPE * H;
-        if (l == 0)
-            add(z, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0, re, ce);
-        else
+        if (l == 0) {
+            add(in.dz0, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0, re, ce);
+            r.job[nj - 1].zrm = 1;
+        } else
             add(z, reinterpret_cast<const __bf16*>(in.eact) + act_off(*edge, in.E, l, 1), 0, RPE, in.E, in.epart, Ge,
                 off, off + (int64_t)n * k, n, k, act_cols(*edge, l), 0, re, ce);
         off += (int64_t)n * k + n;
@@ -2301,7 +2343,7 @@ static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const 
     w.daggr = o;
     o += align_up((size_t)t->num_nodes * H * es);
     w.dz0 = o;
-    o += align_up((size_t)t->num_edges * H * es);
+    o += align_up((size_t)rows_pad(t->num_edges) * H * es);  // chained path: padded rows written (zero)
     w.dP8 = o;
     o += align_up((size_t)2 * rows_pad(t->num_nodes) * H * es);
     w.total = o;
@@ -2402,6 +2444,7 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
         in.aggr = saved->aggr;
         in.eact = saved->edge.act;
         in.edz8 = dz8;
+        in.dz0 = dz0;
         in.dP8 = dP8;
         in.edsp = dsp;
         in.entiles = ntiles;
