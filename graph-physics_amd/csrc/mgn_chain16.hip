@@ -476,6 +476,8 @@ struct BIn16 {  // raw bf16: features 16t + 4g .. +3
     unsigned mask[3];
 };
 
+// ZD: de_out is identically zero (the processor's last block: EncodeProcessDecode returns nodes only)
+template <bool ZD>
 __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
     const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
     const int off = 4 * (lane >> 4);
@@ -484,7 +486,7 @@ __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t 
     const __bf16* z = a.z_save + row * H + off;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-        in.d[t] = *reinterpret_cast<const u32x2*>(d + 16 * t);
+        in.d[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
         in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
         in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
     }
@@ -510,6 +512,7 @@ __device__ __forceinline__ void pin_in(const S& in) {
     for (int l = 0; l < 3; ++l) pin(in.mask[l]);
 }
 
+template <bool ZD>
 __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     const int gi0 = bidx(a, min(tile, last), lane);
     stage16(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
-    bload(nxt, a, min(tile, last), gi0, lane);
+    bload<ZD>(nxt, a, min(tile, last), gi0, lane);
     for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
     __syncthreads();
     // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
         for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
         STAMP(1);
-        bload(nxt, a, min(tile + stride, last), ngi, lane);
+        bload<ZD>(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
         bf16x8 B[4];
         to_operand(acc, B);
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             if (l == 1) {
                 const __bf16* d = a.dout + clamp_row(row, a.M) * H + 4 * g;
 #pragma unroll
-                for (int t = 0; t < 8; ++t) dre[t] = *reinterpret_cast<const u32x2*>(d + 16 * t);
+                for (int t = 0; t < 8; ++t) dre[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
             }
             // stores its B operand dZ_l (R8) under the MFMAs
             gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
@@ -607,7 +610,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         gemm16_st(acc, W, 0, B, lane, scr, StoreDst{nullptr, a.dz0}, tile, a.RP);
         STAMP(6);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] += bf4(dre[t]);
+        for (int t = 0; t < 8; ++t)
+            if (!ZD) acc[t] += bf4(dre[t]);
         store_rows(acc, scr, a.de, tile, a.M, lane);
         STAMP(7);
         pin_in(nxt);
@@ -993,11 +997,12 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.dz0 = reinterpret_cast<__bf16*>(dz0);
     *nparts = 0;
     if (a.ntiles == 0) return 0;
-    if (int e2 = set_lds_once((const void*)chain16_bwd_kernel, LDS_TOTAL)) return e2;
+    const auto kern = dout ? chain16_bwd_kernel<false> : chain16_bwd_kernel<true>;
+    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
     const int grid = chain16_grid(a.ntiles);
     *nparts = grid;
     ProfScope ps(PROF_BWD_EDGE, st);
-    hipLaunchKernelGGL(chain16_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

@@ -2361,6 +2361,8 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     if (int r = check_mlp(node)) return r;
     const BlockWs wl = block_ws_parts(t, edge, node);
     MGN_REQUIRE(ws_bytes >= wl.total, "block backward workspace too small");
+    MGN_REQUIRE(de_out || t->num_edges == 0 || (chain_eligible(edge) && chain_variant() == 16),
+                "de_out = NULL (zero edge-output gradient) needs the chained bf16 h=128 edge MLP");
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
     char* w = reinterpret_cast<char*>(ws);

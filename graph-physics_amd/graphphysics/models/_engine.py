@@ -382,8 +382,12 @@ class EPDFunction(torch.autograd.Function):
             g = gout.detach().float().contiguous()
             _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                      ctypes.c_void_p(gp + 4 * off[2]), ws, st)
-        de = torch.zeros((E, H), dtype=tdt, device=dev)
         nb = len(bdescs) // 2
+        # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
+        # gradient is zero, which the chained bf16 kernels take as NULL (no zero fill, no reads)
+        de = None if nb and nat.lib().mgn_block_forward_inference_supported(
+            ctypes.byref(bdescs[2 * nb - 2]), ctypes.byref(bdescs[2 * nb - 1])) else \
+            torch.zeros((E, H), dtype=tdt, device=dev)
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
             de1 = torch.empty((E, H), dtype=tdt, device=dev)

@@ -157,7 +157,9 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
 size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
                                           const mgn_mlp* node);
 /* dx/de: gradients w.r.t. the block inputs (overwritten). edge_grads/node_grads: flat fp32 as
- * in mgn_mlp_backward (overwritten). */
+ * in mgn_mlp_backward (overwritten). de_out may be NULL (a zero edge-output gradient: the last
+ * processor block, whose e' EncodeProcessDecode discards) where
+ * mgn_block_forward_inference_supported() is 1. */
 int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
                        const void* x, const void* e, const mgn_block_saved* saved,
                        const void* dx_out, const void* de_out, void* dx, void* de,
