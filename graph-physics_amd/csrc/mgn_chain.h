@@ -113,3 +113,11 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
                           hipStream_t st);
 // which chained variant block forward/backward use (read once; env MGN_CHAIN=32 or 16)
 int chain_variant();
+// dense MLP in_dim <= 32 -> 128 -> 128 -> 128 -> 128 + RMSNorm, bf16 (the encoders): 16-row chained
+// kernels with the generic DENSE save layout (ReLU masks: chained lane words)
+bool chain_dense_eligible(const mgn_mlp* m);
+int chain16_dense_forward(const mgn_mlp* m, const void* in, int in_dtype, int64_t in_ld, const int32_t* in_rows,
+                          int64_t M, void* out, int out_dtype, mgn_mlp_saved* sv, hipStream_t st);
+int chain16_dense_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, int dout_dtype,
+                           void* din, int din_dtype, int64_t din_ld, void* dz8, float* dscale_part, int* nparts,
+                           hipStream_t st);

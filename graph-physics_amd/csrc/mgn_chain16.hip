@@ -15,6 +15,7 @@
 #include <utility>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "mgn_chain.h"
 
@@ -924,6 +925,326 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     }
 }
 
+// ------------------------------------------------------------------------------------ dense MLP (encoders)
+// build_mlp(in_dim ≤ 32, 128, 128, 4) + RMSNorm with no residual: the node and edge encoders
+// (reference processors.py:72-82, applied at 127-128). Layer 0 is ONE 16x16x32 k-step per output
+// tile (input columns zero-padded to 32; weights from the LDS image's slot 0, k-step 0); layers 1-3
+// and the RMSNorm as in the block kernels. Saves follow the generic DENSE layout (R8 inputs of every
+// layer incl. the padded layer-0 input, z, rden), so the generic weight-gradient kernel consumes
+// them; the ReLU masks are the chained lane words (forward and backward are both chained whenever
+// chain_dense_eligible(m), so the two always agree).
+struct ChainDenseFwdArgs {
+    const void* in;             // [*][in_ld] fp32 or bf16 MLP input
+    const int32_t* in_rows;     // optional row gather
+    int64_t in_ld;
+    int32_t K0, in_f32, out_f32, pad;
+    const __bf16* wpack;
+    int64_t woff[4];
+    int32_t wks[4];
+    const float* bias[4];
+    const float* scale;
+    float dinv;
+    int64_t M, ntiles;
+    void* out;                  // [M][128] bf16 or fp32
+    __bf16* z_save;
+    float* rden_save;
+    __bf16* act8;
+    int64_t act_off[4];         // act_off(m, M, l, 0): layer 0 = R8 [RP][32]
+    unsigned* mask32;
+    int64_t mask_stride;        // 64-bit words per layer
+};
+
+struct ChainDenseBwdArgs {
+    const void* dout;           // [M][128] bf16 or fp32 (template F32D)
+    const __bf16* z_save;
+    const float* rden_save;
+    const float* scale;
+    float dinv;
+    const unsigned* mask32;
+    int64_t mask_stride;
+    const __bf16* wtpack;
+    int64_t woff[4];
+    int32_t wks[4];
+    int64_t M, ntiles;
+    __bf16* dz8;                // R8 [4][RP][128]: dZ of every layer
+    int64_t RP;
+    float* dscale_part;         // [grid][128]
+    void* din;                  // optional [M][din_ld] gradient w.r.t. the (gathered) input rows
+    int32_t din_f32, K0;
+    int64_t din_ld;
+};
+
+// layer-0 B operand of a 16-row tile: lane (m, g) element j = input feature 16(j>>2) + 4g + (j&3)
+// of row m (0 past K0 and past the last row)
+__device__ __forceinline__ bf16x8 dense_in(const ChainDenseFwdArgs& a, int64_t tile, int lane) {
+    const int64_t row = tile * TR + (lane & 15);
+    const bool ok = row < a.M;
+    const int64_t r = clamp_row(row, a.M);
+    const int64_t src = a.in_rows ? (int64_t)a.in_rows[r] : r;
+    const int g = lane >> 4;
+    bf16x8 b;
+    if (a.in_f32) {
+        const float* p = reinterpret_cast<const float*>(a.in) + src * a.in_ld;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = 16 * (j >> 2) + 4 * g + (j & 3);
+            b[j] = (__bf16)(ok && f < a.K0 ? p[f] : 0.f);
+        }
+    } else {
+        const __bf16* p = reinterpret_cast<const __bf16*>(a.in) + src * a.in_ld;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int f = 16 * (j >> 2) + 4 * g + (j & 3);
+            b[j] = ok && f < a.K0 ? p[f] : (__bf16)0.f;
+        }
+    }
+    return b;
+}
+
+__global__ __launch_bounds__(NW * 64) void chain16_dense_fwd_kernel(ChainDenseFwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // bias[4][H], scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    const int m = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t last = a.ntiles - 1;
+    bf16x8 nxt = dense_in(a, min(tile, last), lane);
+    // layer 0's pack has one k-step per output tile: slot 0's k-steps 1..3 receive in-bounds bytes
+    // of the rest of its region that no GEMM reads
+    stage16(W, a.wpack, a.woff, a.wks, false);
+    for (int i = threadIdx.x; i < 5 * H; i += NW * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
+    __syncthreads();
+    if (tile >= a.ntiles) return;
+    pin(nxt);
+    for (; tile < a.ntiles; tile += stride) {
+        const bf16x8 in0 = nxt;
+        nxt = dense_in(a, min(tile + stride, last), lane);
+        const int64_t row = tile * TR + m;
+        // padded layer-0 input as R8 [RP][32] (operand of W0's weight gradient): the tile's 16 x 32
+        // block through the scratch, then lane (u, c) stores rows 8u..8u+7 of column c (16 bytes)
+        {
+            constexpr int LD0 = 40;
+            const u32x4 w = __builtin_bit_cast(u32x4, in0);
+            *reinterpret_cast<u32x2*>(scr + m * LD0 + 4 * g) = u32x2{w[0], w[1]};
+            *reinterpret_cast<u32x2*>(scr + m * LD0 + 16 + 4 * g) = u32x2{w[2], w[3]};
+            lds_fence();
+            const int u = lane >> 5, c = lane & 31;
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = scr[(8 * u + q) * LD0 + c];
+            lds_fence();  // scratch free for the layer saves below
+            *reinterpret_cast<bf16x8*>(a.act8 + a.act_off[0] + (((int64_t)tile * 2 + u) * 32 + c) * 8) = o;
+        }
+        f4 acc[8];
+        bf16x8 B[4];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            if (l == 0) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, 0, t, 0, lane), in0, f4{0.f, 0.f, 0.f, 0.f});
+            } else {
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
+            }
+            unsigned bits = 0u;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f4 b = *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = fmaxf(acc[t][r] + b[r], 0.f);
+                    acc[t][r] = v;
+                    bits = push_bit(bits, v);
+                }
+            }
+            to_operand(acc, B);
+            a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
+        }
+        gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float z = acc[t][r] + b[r];
+                acc[t][r] = z;
+                ss = fmaf(z, z, ss);
+            }
+        }
+        ss += __shfl_xor(ss, 16);
+        ss += __shfl_xor(ss, 32);
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        const float rq = __builtin_amdgcn_rcpf(q);
+        if (g == 0 && row < a.M) a.rden_save[row] = q;
+        store_rows(acc, scr, a.z_save, tile, a.M, lane);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[t][r] = s[r] * (acc[t][r] * rq);
+        }
+        if (a.out_f32) {
+            if (row < a.M) {
+                float* o = reinterpret_cast<float*>(a.out) + row * H + 4 * g;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(o + 16 * t) = acc[t];
+            }
+        } else {
+            store_rows(acc, scr, reinterpret_cast<__bf16*>(a.out), tile, a.M, lane);
+        }
+        pin(nxt);
+    }
+}
+
+template <bool F32D>
+struct DIn16 {
+    typename std::conditional<F32D, f4, u32x2>::type d[8];  // dout[row]: fp32, or raw bf16 pairs
+    u32x2 z[8];
+    float q;
+    unsigned mask[3];
+};
+
+template <bool F32D>
+__device__ __forceinline__ void dload(DIn16<F32D>& in, const ChainDenseBwdArgs& a, int64_t tile, int lane) {
+    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
+    const int off = 4 * (lane >> 4);
+    const __bf16* z = a.z_save + row * H + off;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        if constexpr (F32D)
+            in.d[t] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(a.dout) + row * H + off + 16 * t);
+        else
+            in.d[t] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const __bf16*>(a.dout) + row * H + off + 16 * t);
+        in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
+    }
+    in.q = a.rden_save[row];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) in.mask[l] = a.mask32[l * a.mask_stride * 2 + tile * 64 + lane];
+}
+
+template <bool F32D>
+__device__ __forceinline__ void dpin(const DIn16<F32D>& in) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        pin(in.d[t]);
+        pin(in.z[t]);
+    }
+    pin(in.q);
+#pragma unroll
+    for (int l = 0; l < 3; ++l) pin(in.mask[l]);
+}
+
+template <bool F32D>
+__global__ __launch_bounds__(NW * 64) void chain16_dense_bwd_kernel(ChainDenseBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __bf16* W = reinterpret_cast<__bf16*>(smem);
+    float* vec = reinterpret_cast<float*>(smem + LDS_W);  // scale[H]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
+    const int m = lane & 15, g = lane >> 4;
+    const int r4 = 2 * (m & 1) + ((m >> 1) & 1);  // row16_sum4's component in lane m
+    const int64_t stride = (int64_t)gridDim.x * NW;
+    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t last = a.ntiles - 1;
+    stage16(W, a.wtpack, a.woff, a.wks, true);
+    DIn16<F32D> nxt;
+    dload<F32D>(nxt, a, min(tile, last), lane);
+    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
+    for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
+    __syncthreads();
+    if (tile < a.ntiles) dpin<F32D>(nxt);
+    for (; tile < a.ntiles; tile += stride) {
+        const int64_t row = tile * TR + m;
+        const bool ok = row < a.M;
+        // RMSNorm backward (layers.py:59-74), as chain16_bwd_kernel without the aggregate term
+        f4 acc[8];
+        float dot = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            f4 dy;
+            if constexpr (F32D)
+                dy = nxt.d[t];
+            else
+                dy = bf4(nxt.d[t]);
+            const f4 z = bf4(nxt.z[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            acc[t] = dy;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dot = fmaf(sc[r] * dy[r], z[r], dot);
+        }
+        dot += __shfl_xor(dot, 16);
+        dot += __shfl_xor(dot, 32);
+        const float qd = nxt.q;
+        const float rq = __builtin_amdgcn_rcpf(qd);
+        const float rms = qd - RMS_EPS;
+        const float coef = rms > 0.f ? dot / (qd * qd * rms) * (a.dinv * a.dinv) : 0.f;
+        const int okm = ok ? -1 : 0;  // bit mask, not a select (see chain16_bwd_kernel)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f4 z = bf4(nxt.z[t]);
+            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            f4 ds;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dy = acc[t][r];
+                acc[t][r] = __int_as_float(__float_as_int(fmaf(-z[r], coef, sc[r] * dy * rq)) & okm);
+                ds[r] = __int_as_float(__float_as_int(dy * z[r] * rq) & okm);
+            }
+            const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
+            if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
+        }
+        unsigned mcur[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
+        dload<F32D>(nxt, a, min(tile + stride, last), lane);
+        bf16x8 B[4];
+        to_operand(acc, B);
+        // layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]; each GEMM stores its B operand dZ_l (R8)
+#pragma unroll
+        for (int l = 3; l >= 1; --l) {
+            gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
+            relu_mask(acc, mcur[l - 1]);
+            to_operand(acc, B);
+        }
+        store_r8(acc, scr, a.dz8, tile, lane);  // dZ0: operand of W0's weight gradient
+        if (a.din) {
+            // dA0 = dZ0 · W0 (transposed image slot 0): output tiles 0-1 = input features 0..31
+            f4 d2[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) d2[t] = mfma16(wfrag(W, 0, t, s, lane), B[s], d2[t]);
+            if (ok) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int k = 16 * t + 4 * g + r;
+                        if (k < a.K0) {
+                            if (a.din_f32)
+                                reinterpret_cast<float*>(a.din)[row * a.din_ld + k] = d2[t][r];
+                            else
+                                reinterpret_cast<__bf16*>(a.din)[row * a.din_ld + k] = (__bf16)d2[t][r];
+                        }
+                    }
+            }
+        }
+        dpin<F32D>(nxt);
+    }
+    // dscale partials of the workgroup: the waves' rows in wave order
+    __syncthreads();
+    if (threadIdx.x < H) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s += red[w * H + threadIdx.x];
+        a.dscale_part[(int64_t)blockIdx.x * H + threadIdx.x] = s;
+    }
+}
+
 int set_lds_once(const void* fn, size_t bytes) {
     static std::mutex mu;
     static const void* done[16] = {};
@@ -1079,6 +1400,84 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
     hipLaunchKernelGGL(chain16_node_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+// the encoders' shape on the chained kernels (env MGN_CHAIN_DENSE=0: generic kernels, for A/B);
+// read once, like chain_variant(): forward and backward must agree on the ReLU-mask layout
+bool chain_dense_eligible(const mgn_mlp* m) {
+    static const bool on = [] {
+        const char* e = getenv("MGN_CHAIN_DENSE");
+        return !(e && atoi(e) == 0);
+    }();
+    return on && m->dtype == MGN_BF16 && m->hidden == H && m->out_dim == H && m->n_layers == 4 && m->has_norm &&
+           m->in_dim >= 1 && m->in_dim <= 32 && chain_variant() == 16;
+}
+
+int chain16_dense_forward(const mgn_mlp* m, const void* in, int in_dtype, int64_t in_ld, const int32_t* in_rows,
+                          int64_t M, void* out, int out_dtype, mgn_mlp_saved* sv, hipStream_t st) {
+    ChainDenseFwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = in;
+    a.in_rows = in_rows;
+    a.in_ld = in_ld;
+    a.K0 = m->in_dim;
+    a.in_f32 = in_dtype == MGN_F32;
+    a.out_f32 = out_dtype == MGN_F32;
+    a.wpack = reinterpret_cast<const __bf16*>(m->wpack);
+    layer_offsets(m, a.woff, a.wks);
+    for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;
+    a.out = out;
+    a.z_save = reinterpret_cast<__bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.act8 = reinterpret_cast<__bf16*>(sv->act);
+    for (int l = 0; l < 4; ++l) a.act_off[l] = act_off(*m, M, l, 0);
+    a.mask32 = reinterpret_cast<unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    if (a.ntiles == 0) return 0;
+    if (int e2 = set_lds_once((const void*)chain16_dense_fwd_kernel, LDS_TOTAL)) return e2;
+    ProfScope ps(PROF_FWD_DENSE, st);
+    hipLaunchKernelGGL(chain16_dense_fwd_kernel, dim3(chain16_grid(a.ntiles)), dim3(NW * 64), LDS_TOTAL, st, a);
+    MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int chain16_dense_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, int dout_dtype,
+                           void* din, int din_dtype, int64_t din_ld, void* dz8, float* dscale_part, int* nparts,
+                           hipStream_t st) {
+    ChainDenseBwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dout = dout;
+    a.z_save = reinterpret_cast<const __bf16*>(sv->z);
+    a.rden_save = sv->rden;
+    a.scale = m->scale;
+    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
+    a.mask_stride = mask_words_per_layer(*m, M);
+    a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
+    layer_offsets(m, a.woff, a.wks);
+    a.M = M;
+    a.ntiles = rows_pad(M) / TR;
+    a.dz8 = reinterpret_cast<__bf16*>(dz8);
+    a.RP = rows_pad(M);
+    a.dscale_part = dscale_part;
+    a.din = din;
+    a.din_f32 = din_dtype == MGN_F32;
+    a.K0 = m->in_dim;
+    a.din_ld = din_ld;
+    *nparts = 0;
+    if (a.ntiles == 0) return 0;
+    const auto kern = dout_dtype == MGN_F32 ? chain16_dense_bwd_kernel<true> : chain16_dense_bwd_kernel<false>;
+    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
+    const int grid = chain16_grid(a.ntiles);
+    *nparts = grid;
+    ProfScope ps(PROF_BWD_DENSE, st);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

@@ -2215,6 +2215,8 @@ int mgn_mlp_forward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t 
     MGN_REQUIRE(saved && saved->act && (m->n_layers < 2 || saved->mask) && (!m->has_norm || (saved->z && saved->rden)),
                 "saved buffers missing");
     MGN_REQUIRE(in_dtype == MGN_F32 || in_dtype == m->dtype, "input dtype must be fp32 or the MLP dtype");
+    if (chain_dense_eligible(m))
+        return chain16_dense_forward(m, in, in_dtype, in_ld, in_rows, rows, out, out_dtype, saved, (hipStream_t)stream);
     MlpIn mi;
     memset(&mi, 0, sizeof(mi));
     mi.seg[0] = SrcSeg{in, in_rows, in_ld, m->in_dim, in_dtype, 0, 0};
@@ -2236,6 +2238,25 @@ int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t
                      int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,
                      int32_t din_dtype, float* grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
     if (int e = check_mlp(m)) return e;
+    if (chain_dense_eligible(m) && rows > 0) {
+        // chained data gradients (dZ of every layer, din) + the generic weight gradients over the
+        // same R8 operands; workspace carve as mlp_backward_impl: dz | dscale partials | slabs
+        MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, rows), "backward workspace too small");
+        MGN_REQUIRE(dout_dtype == MGN_F32 || dout_dtype == MGN_BF16, "dout dtype must be MGN_F32 or MGN_BF16");
+        hipStream_t st = (hipStream_t)stream;
+        const int ntiles = (int)(rows_pad(rows) / bm_host(m->dtype, MODE_DENSE));
+        char* p = reinterpret_cast<char*>(ws);
+        void* dz = p;
+        p += align_up((size_t)m->n_layers * rows_pad(rows) * m->hidden * 2);
+        float* dsp = reinterpret_cast<float*>(p);
+        p += align_up((size_t)ntiles * m->out_dim * sizeof(float));
+        float* part = reinterpret_cast<float*>(p);
+        int nparts = 0;
+        if (int e = chain16_dense_backward(m, rows, saved, dout, dout_dtype, din, din_dtype, m->in_dim, dz, dsp,
+                                           &nparts, st))
+            return e;
+        return mlp_wgrad_any(m, rows, saved->act, dz, dsp, nparts, part, grads, nullptr, 0, nullptr, true, st);
+    }
     MlpIn mi;
     memset(&mi, 0, sizeof(mi));
     mi.seg[0] = SrcSeg{in, in_rows, in_ld, m->in_dim, in_dtype, 0, 0};

@@ -111,3 +111,53 @@ def cylinder_batch(batch, t=0, jitter=0.0, seed=1234, mesh=None):
         "num_graphs": batch,
         "nodes_per_graph": n,
     }
+
+
+OBSTACLE, HANDLE = 1, 3  # reference graphphysics/utils/nodetype.py
+
+
+def tet_grid(nx, ny, nz, spacing, origin=(0.0, 0.0, 0.0)):
+    """Structured tetrahedral mesh of an nx × ny × nz node grid: each cube split into the 6 Kuhn
+    tetrahedra around its main diagonal. Returns pos [N,3] float32, cells [6·cubes, 4] int64."""
+    ii, jj, kk = np.meshgrid(np.arange(nx), np.arange(ny), np.arange(nz), indexing="ij")
+    pos = np.stack([ii, jj, kk], -1).reshape(-1, 3) * spacing + np.asarray(origin)
+    vid = lambda i, j, k: (i * ny + j) * nz + k  # noqa: E731
+    i, j, k = [a.reshape(-1) for a in np.meshgrid(np.arange(nx - 1), np.arange(ny - 1), np.arange(nz - 1),
+                                                   indexing="ij")]
+    v = {(a, b, c): vid(i + a, j + b, k + c) for a in (0, 1) for b in (0, 1) for c in (0, 1)}
+    tets = [(v[0, 0, 0], v[1, 0, 0], v[1, 1, 0], v[1, 1, 1]), (v[0, 0, 0], v[1, 0, 0], v[1, 0, 1], v[1, 1, 1]),
+            (v[0, 0, 0], v[0, 1, 0], v[1, 1, 0], v[1, 1, 1]), (v[0, 0, 0], v[0, 1, 0], v[0, 1, 1], v[1, 1, 1]),
+            (v[0, 0, 0], v[0, 0, 1], v[1, 0, 1], v[1, 1, 1]), (v[0, 0, 0], v[0, 0, 1], v[0, 1, 1], v[1, 1, 1])]
+    cells = np.concatenate([np.stack(t, 1) for t in tets], 0)
+    return pos.astype(np.float32), cells.astype(np.int64)
+
+
+def plate_sample(seed=0, nx=25, ny=13, nz=4, spacing=0.04):
+    """DeformingPlate-shaped frame pair (SURVEY.md §8 Cfg C; the dataset is not in-tree): a tet-meshed
+    plate (nx·ny·nz nodes, the x = 0 face HANDLE, the rest NORMAL) and a small tet-meshed OBSTACLE
+    block 0.02 above its top face, pressing down. Raw layout of the reference's plate frames before
+    preprocessing: x = [world_pos(3), node_type], y = next world_pos, pos = mesh_pos, cells [F, 4].
+    With build_preprocessing(world_pos_parameters={0, 3, node_type_index 6}) this gives the model's
+    node_in 6 + 9, edge_in 3 + 1 + 3 + 1 = 8 (plate.json indices, preprocessing.py:49-174)."""
+    rng = np.random.default_rng(seed)
+    ppos, pcells = tet_grid(nx, ny, nz, spacing)
+    top = ppos[:, 2].max()
+    cx, cy = ppos[:, 0].mean(), ppos[:, 1].mean()
+    opos, ocells = tet_grid(5, 5, 2, 0.02, origin=(cx - 0.04, cy - 0.04, top + 0.02))
+    n_p = ppos.shape[0]
+    mesh_pos = np.concatenate([ppos, opos], 0)
+    cells = np.concatenate([pcells, ocells + n_p], 0)
+    nt = np.full(mesh_pos.shape[0], NORMAL, np.float32)
+    nt[:n_p][ppos[:, 0] == 0] = HANDLE
+    nt[n_p:] = OBSTACLE
+    # current world positions: a small seeded bend of the plate; next frame: the obstacle moves down,
+    # plate nodes follow with a smooth displacement, handles stay
+    world = mesh_pos.copy()
+    world[:n_p, 2] += 0.005 * np.sin(np.pi * ppos[:, 0] / ppos[:, 0].max()) * rng.uniform(0.5, 1.5)
+    nxt = world.copy()
+    nxt[n_p:, 2] -= 0.003
+    r = np.hypot(world[:n_p, 0] - cx, world[:n_p, 1] - cy)
+    nxt[:n_p, 2] -= 0.002 * np.exp(-(r / 0.1) ** 2) * (nt[:n_p] == NORMAL)
+    nxt[:n_p] += 1e-4 * rng.standard_normal((n_p, 3)) * (nt[:n_p, None] == NORMAL)
+    x = np.concatenate([world, nt[:, None]], 1).astype(np.float32)
+    return {"x": x, "y": nxt.astype(np.float32), "pos": mesh_pos.astype(np.float32), "cells": cells}

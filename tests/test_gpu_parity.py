@@ -567,3 +567,62 @@ def test_block_bf16_h128_multi_tile_and_padding(nb, trim):
         # test_block_cylinder_h128_vs_oracle (0.15 on gradients, measured up to ~0.10). A padding
         # or tiling bug shows up as non-finite or O(1) errors.
         assert relerr(v, res[torch.float32][k]) < 0.15, (k, relerr(v, res[torch.float32][k]))
+
+
+@pytest.mark.parametrize("rows,in_dim,gather,out_f32,din", [(88560, 3, True, False, False),
+                                                           (15384, 11, False, False, True),
+                                                           (37, 3, True, True, True), (1, 23, False, True, True)])
+def test_encoder_mlp_bf16_chained_vs_fp64(rows, in_dim, gather, out_f32, din):
+    """The chained bf16 dense MLP (the encoders: in_dim ≤ 32 → 128, 4 Linears + RMSNorm) through
+    mgn_mlp_forward / mgn_mlp_backward — Cfg B edge-encoder rows with the CSC row gather, node-encoder
+    rows with the input gradient, a ragged tile and a single row: no further from an fp64 evaluation
+    of build_mlp than 2 × PyTorch's own bf16 autocast of it (floor 1e-2)."""
+    import copy
+    import ctypes
+
+    from graphphysics import _native as nat
+    from graphphysics.models import _engine
+    from graphphysics.models.layers import build_mlp
+
+    torch.manual_seed(0)
+    mlp = build_mlp(in_dim, 128, 128, 4, True)
+    ref = copy.deepcopy(mlp)
+    mlp = mlp.to(DEV)
+    plan = _engine.ModelPlan(mlp, [mlp])
+    pw = plan.packed(DEV, nat.MGN_BF16)
+    st = nat.stream_ptr(DEV)
+    pw.repack(st)
+    desc, spec = pw.descs[0], plan.specs[0]
+    g = torch.Generator().manual_seed(3)
+    src_rows = rows + 5 if gather else rows
+    x = torch.randn(src_rows, in_dim, generator=g)
+    idx = torch.randperm(src_rows, generator=g)[:rows].int() if gather else None
+    odt = torch.float32 if out_f32 else torch.bfloat16
+    gout = torch.randn(rows, 128, generator=g).to(odt)
+    xd, idd = x.to(DEV), (idx.to(DEV) if gather else None)
+    sv, keep = _engine._alloc_mlp_saved(desc, spec, rows, torch.bfloat16, DEV, True)
+    out = torch.empty(rows, 128, dtype=odt, device=DEV)
+    mo = nat.MGN_F32 if out_f32 else nat.MGN_BF16
+    _engine._mlp_fwd(desc, spec, xd, nat.MGN_F32, in_dim, idd, rows, out, mo, sv, st)
+    ws = torch.empty(_engine._ws_bytes_mlp(desc, rows), dtype=torch.uint8, device=DEV)
+    G = torch.empty(plan.numel, device=DEV)
+    dind = torch.empty(rows, in_dim, device=DEV) if din else None
+    _engine._mlp_bwd(desc, xd, nat.MGN_F32, in_dim, idd, rows, sv, gout.to(DEV), mo, dind, nat.MGN_F32,
+                     ctypes.c_void_p(G.data_ptr()), ws, st)
+    torch.cuda.synchronize()
+    xin = x[idx.long()] if gather else x
+    x64 = xin.double().requires_grad_(True)
+    m64 = copy.deepcopy(ref).double()
+    (m64(x64) * gout.double()).sum().backward()
+    y64 = m64(x64.detach())
+    xac = xin.clone().requires_grad_(True)
+    mac = copy.deepcopy(ref)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = mac(xac)
+    (yac.float() * gout.float()).sum().backward()
+    assert torch.isfinite(out.float()).all()
+    assert relerr(out, y64) <= max(1e-2, 2 * relerr(yac, y64))
+    for (k, p64), pa, gg in zip(m64.named_parameters(), mac.parameters(), plan.grad_views(G)):
+        assert relerr(gg, p64.grad) <= max(1e-2, 2 * relerr(pa.grad, p64.grad)), k
+    if din:
+        assert relerr(dind, x64.grad) <= max(1e-2, 2 * relerr(xac.grad, x64.grad))
