@@ -89,23 +89,6 @@ struct ChainNodeBwdArgs {
     float* dscale_part;
     __bf16* dx_part;            // dx_out + dA0[:, :128]
     __bf16* d_aggr;             // dA0[:, 128:]
-    // FUSED (mgn_processor_backward): dx_out is the NEXT block's pending data gradient, formed here
-    // instead of by its node_grad launch: dx_out = n_dx_part + [Σ_in n_dz0 ‖ Σ_out n_dz0]·W0[:, h:3h]
-    const __bf16* n_dz0;        // [RP_E][128] its edge layer-0 dZ (target-sorted rows)
-    const __bf16* n_dx_part;    // [N][128]
-    const __bf16* n_wt0;        // its edge MLP's transposed layer-0 fragments ([3h x h])
-    const int32_t* col_ptr;     // CSC in-edge segments
-    const int32_t* row_ptr;     // out-edge segments (source-sorted) ...
-    const int32_t* row_perm;    // ... as target-sorted positions
-    __bf16* n_dP8;              // R8 [2][RP][128]: its dP_i, dP_j (weight-gradient operands)
-};
-
-// the next block's node-side gradient inputs, folded into a node-MLP backward (see above)
-struct PendingDx {
-    const void* dz0;
-    const void* dx_part;
-    const void* wt0;
-    void* dP8;
 };
 
 bool chain_eligible(const mgn_mlp* m);
@@ -114,8 +97,7 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
                          hipStream_t st);
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
-                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st,
-                          const mgn_topology* t = nullptr, const PendingDx* pend = nullptr);
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
 int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
                        int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
 // nparts: number of dscale partial rows written (the reduction's row count)

@@ -818,35 +818,6 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     STAMP_PRINT("nfwd16");
 }
 
-// Σ_{k ∈ [kb, ke)} rows[perm ? perm[k] : k] in the accumulator layout (the lane's 32 features of its
-// node), in edge order: the order (and the fp32 adds of bf16 rows) of node_grad_kernel's segment sums
-__device__ __forceinline__ void seg_rows16(f4 (&s)[8], const __bf16* rows, const int32_t* perm, int kb, int ke,
-                                           int g) {
-    constexpr int AG = 4;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) s[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int k = kb; k < ke; k += AG) {
-        u32x2 zz[AG][8];
-#pragma unroll
-        for (int u = 0; u < AG; ++u) {
-            const int ku = k + u < ke ? k + u : ke - 1;  // past the segment: reload its last row, add 0
-            const int64_t r = perm ? (int64_t)perm[ku] : (int64_t)ku;
-            const __bf16* zp = rows + r * H + 4 * g;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) zz[u][t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
-        }
-#pragma unroll
-        for (int u = 0; u < AG; ++u) {
-            const float w = k + u < ke ? 1.f : 0.f;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) s[t] += bf4(zz[u][t]) * w;
-        }
-    }
-}
-
-// FUSED: dx_out is not read but formed from the next block's pending gradient (ChainNodeBwdArgs)
-template <bool FUSED>
 __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -868,63 +839,13 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         const bool ok = row < a.M;
         const int64_t v = clamp_row(row, a.M);
         u32x2 d[8], zr[8];
-        f4 dyo[8];  // FUSED: dx_out of this tile in fp32
-        if constexpr (FUSED) {
-            // the next block's node_grad, folded in: dP_i = Σ_in dZ0, dP_j = Σ_out dZ0 (R8 saves for
-            // its weight gradient), dx_out = dx_part + W0bᵀ·dP_i + W0cᵀ·dP_j (its transposed edge W0,
-            // input-feature tiles 8..15 and 16..23, from L2)
-            const int kbi = a.col_ptr[v], kei = ok ? a.col_ptr[v + 1] : kbi;
-            const int kbj = a.row_ptr[v], kej = ok ? a.row_ptr[v + 1] : kbj;
-            bf16x8 Bi[4], Bj[4];
-            {
-                f4 dp8[8];
-                seg_rows16(dp8, a.n_dz0, nullptr, kbi, kei, g);
-                store_r8(dp8, scr, a.n_dP8, tile, lane);
-                to_operand(dp8, Bi);
-                seg_rows16(dp8, a.n_dz0, a.row_perm, kbj, kej, g);
-                store_r8(dp8, scr, a.n_dP8 + a.RP * H, tile, lane);
-                to_operand(dp8, Bj);
-            }
-            u32x2 xp[8];
-            const __bf16* pp = a.n_dx_part + v * H + 4 * g;
-            const __bf16* zp = a.z_save + v * H + 4 * g;
+        const __bf16* dp = a.dout + v * H + 4 * g;
+        const __bf16* zp = a.z_save + v * H + 4 * g;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                xp[t] = *reinterpret_cast<const u32x2*>(pp + 16 * t);
-                zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
-            }
-            const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.n_wt0);
-            const int vo = gfrag_voff(lane);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) dyo[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int blk = 0; blk < 2; ++blk) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    bf16x8 fr[8];
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) fr[t] = gfrag(rs, vo, (8 + 8 * blk + t) * 4 + s);
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) dyo[t] = mfma16(fr[t], blk ? Bj[s] : Bi[s], dyo[t]);
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 8; ++t) dyo[t] = bf4(xp[t]) + dyo[t];
-        } else {
-            const __bf16* dp = a.dout + v * H + 4 * g;
-            const __bf16* zp = a.z_save + v * H + 4 * g;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
-                zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
-            }
+        for (int t = 0; t < 8; ++t) {
+            d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
+            zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
         }
-        auto dy_of = [&](int t) -> f4 {
-            if constexpr (FUSED)
-                return dyo[t];
-            else
-                return bf4(d[t]);
-        };
         const float qd = a.rden_save[v];
         unsigned mk[3];
 #pragma unroll
@@ -934,7 +855,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         float dot = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            const f4 dy = dy_of(t);
+            const f4 dy = bf4(d[t]);
             const f4 z = bf4(zr[t]);
             const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
             acc[t] = dy;
@@ -975,7 +896,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
         gemm16(acc, W, 0, B, lane);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] += dy_of(t);
+        for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
         store_rows(acc, scr, a.dx_part, tile, a.M, lane);
         {
             const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
@@ -1453,8 +1374,7 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
 }
 
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
-                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st,
-                          const mgn_topology* t, const PendingDx* pend) {
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st) {
     ChainNodeBwdArgs a;
     memset(&a, 0, sizeof(a));
     a.dout = reinterpret_cast<const __bf16*>(dout);
@@ -1473,23 +1393,13 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.dscale_part = dscale_part;
     a.dx_part = reinterpret_cast<__bf16*>(dx_part);
     a.d_aggr = reinterpret_cast<__bf16*>(d_aggr);
-    if (pend) {
-        a.n_dz0 = reinterpret_cast<const __bf16*>(pend->dz0);
-        a.n_dx_part = reinterpret_cast<const __bf16*>(pend->dx_part);
-        a.n_wt0 = reinterpret_cast<const __bf16*>(pend->wt0);
-        a.n_dP8 = reinterpret_cast<__bf16*>(pend->dP8);
-        a.col_ptr = t->col_ptr;
-        a.row_ptr = t->row_ptr;
-        a.row_perm = t->row_perm;
-    }
     *nparts = 0;
     if (M == 0) return 0;
-    const auto kern = pend ? chain16_node_bwd_kernel<true> : chain16_node_bwd_kernel<false>;
-    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
+    if (int e2 = set_lds_once((const void*)chain16_node_bwd_kernel, LDS_TOTAL)) return e2;
     const int grid = node_grid(a.ntiles);
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(chain16_node_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

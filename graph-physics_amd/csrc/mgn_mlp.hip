@@ -2506,129 +2506,4 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     return launch_reduce(edge, part, nchunks, dsp, ntiles, edge_grads, st);
 }
 
-// ---------------------------------------------------------------------------------- processor stack
-// EncodeProcessDecode's processor loop (processors.py:130-131) as one call, so the library can fuse
-// across blocks: block b's node-MLP backward forms block b+1's data gradient itself (its node_grad:
-// segment sums of dZ0 + the x blocks of its edge W0), which therefore never runs as a launch of its
-// own and never round-trips dx through HBM.
-
-int mgn_processor_supported(const mgn_topology* t, int32_t nb, const mgn_mlp* edges, const mgn_mlp* nodes) {
-    if (!t || !edges || !nodes || nb < 1 || t->num_edges <= 0 || t->num_nodes <= 0) return 0;
-    for (int b = 0; b < nb; ++b) {
-        const mgn_mlp* e = &edges[b];
-        const mgn_mlp* n = &nodes[b];
-        if (check_mlp(e) || check_mlp(n)) return 0;
-        if (!(chain_eligible(e) && chain_variant() == 16 && chain_node_eligible(n) && e->in_dim == 3 * e->hidden))
-            return 0;
-    }
-    return 1;
-}
-
-size_t mgn_processor_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
-    // two block workspaces (block b and b+1 are live together) + the second de buffer
-    return 2 * align_up(block_ws_parts(t, edge, node).total) +
-           align_up((size_t)t->num_edges * edge->hidden * (edge->dtype == MGN_F32 ? 4 : 2));
-}
-
-namespace {
-// block b's pieces of a block-backward workspace (the carve of mgn_block_backward, chained path)
-struct BlockBwdBufs {
-    void *dx_part, *d_aggr, *dz0, *dP8, *ndz, *dz8;
-    float *ndsp, *npart, *dsp, *part;
-};
-BlockBwdBufs carve_block_bwd(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, char* w) {
-    const BlockWs wl = block_ws_parts(t, edge, node);
-    const int H = edge->hidden;
-    const int64_t E = t->num_edges, N = t->num_nodes;
-    BlockBwdBufs b;
-    b.dx_part = w + wl.dxpart;
-    b.d_aggr = w + wl.daggr;
-    b.dz0 = w + wl.dz0;
-    b.dP8 = w + wl.dP8;
-    char* q = w + wl.nmlp;
-    b.ndz = q;
-    q += align_up((size_t)node->n_layers * rows_pad(N) * H * 2);
-    b.ndsp = reinterpret_cast<float*>(q);
-    q += align_up((size_t)(rows_pad(N) / 16) * node->out_dim * sizeof(float));
-    b.npart = reinterpret_cast<float*>(q);
-    char* p = w + wl.mlp;
-    b.dz8 = p;
-    p += align_up((size_t)edge->n_layers * rows_pad(E) * H * 2);
-    b.dsp = reinterpret_cast<float*>(p);
-    p += align_up((size_t)(rows_pad(E) / 64) * edge->out_dim * sizeof(float));
-    b.part = reinterpret_cast<float*>(p);
-    return b;
-}
-}  // namespace
-
-int mgn_processor_backward(const mgn_topology* t, int32_t nb, const mgn_mlp* edges, const mgn_mlp* nodes,
-                           const void* const* xs, const void* const* es, const mgn_block_saved* saved,
-                           const void* dx_out, const void* de_out, void* dx, void* de, float* const* edge_grads,
-                           float* const* node_grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
-    MGN_REQUIRE(mgn_processor_supported(t, nb, edges, nodes),
-                "processor stack backward needs every block on the chained bf16 h=128 kernels "
-                "(mgn_processor_supported)");
-    MGN_REQUIRE(xs && es && saved && dx_out && dx && de && edge_grads && node_grads, "processor backward: NULL argument");
-    for (int b = 1; b < nb; ++b)
-        MGN_REQUIRE(block_ws_parts(t, &edges[b], &nodes[b]).total == block_ws_parts(t, &edges[0], &nodes[0]).total,
-                    "processor blocks must share one shape");
-    MGN_REQUIRE(ws_bytes >= mgn_processor_backward_workspace_bytes(t, &edges[0], &nodes[0]),
-                "processor backward workspace too small");
-    hipStream_t st = (hipStream_t)stream;
-    const int64_t E = t->num_edges, N = t->num_nodes;
-    const size_t half = align_up(block_ws_parts(t, &edges[0], &nodes[0]).total);
-    char* w = reinterpret_cast<char*>(ws);
-    void* de_tmp = w + 2 * half;
-    auto bufs = [&](int b) { return carve_block_bwd(t, &edges[b], &nodes[b], w + (b & 1) * half); };
-    auto de_of = [&](int b) -> void* { return (b & 1) ? de_tmp : de; };  // block 0 writes the caller's de
-    int nn[2] = {0, 0}, ne[2] = {0, 0};  // dscale partial rows of blocks b, b+1 (node, edge), by b & 1
-    auto wgrad = [&](int b) {
-        const BlockBwdBufs q = bufs(b);
-        BlockWgradIn in;
-        in.E = E;
-        in.N = N;
-        in.e = es[b];
-        in.x = xs[b];
-        in.aggr = saved[b].aggr;
-        in.eact = saved[b].edge.act;
-        in.edz8 = q.dz8;
-        in.dz0 = q.dz0;
-        in.dP8 = q.dP8;
-        in.edsp = q.dsp;
-        in.entiles = ne[b & 1];
-        in.epart = q.part;
-        in.egrads = edge_grads[b];
-        in.nact = saved[b].node.act;
-        in.ndz8 = q.ndz;
-        in.ndsp = q.ndsp;
-        in.nntiles = nn[b & 1];
-        in.npart = q.npart;
-        in.ngrads = node_grads[b];
-        return block_wgrad_ring(&edges[b], &nodes[b], in, st);
-    };
-    for (int b = nb - 1; b >= 0; --b) {
-        const BlockBwdBufs q = bufs(b);
-        if (b == nb - 1) {
-            if (int r = chain16_node_backward(&nodes[b], N, &saved[b].node, dx_out, q.ndz, q.ndsp, &nn[b & 1],
-                                              q.dx_part, q.d_aggr, st))
-                return r;
-        } else {
-            // block b+1's node_grad folded into block b's node-MLP backward, then block b+1's weights
-            const BlockBwdBufs p = bufs(b + 1);
-            const PendingDx pd{p.dz0, p.dx_part, edges[b + 1].wtpack, p.dP8};
-            if (int r = chain16_node_backward(&nodes[b], N, &saved[b].node, nullptr, q.ndz, q.ndsp, &nn[b & 1],
-                                              q.dx_part, q.d_aggr, st, t, &pd))
-                return r;
-            if (int r = wgrad(b + 1)) return r;
-        }
-        const void* dob = b == nb - 1 ? de_out : de_of(b + 1);
-        if (int r = chain16_edge_backward(&edges[b], E, &saved[b].edge, dob, q.d_aggr, t->csc_dst, q.dz8, q.dsp,
-                                          &ne[b & 1], de_of(b), q.dz0, st))
-            return r;
-    }
-    const BlockBwdBufs q0 = bufs(0);
-    if (int r = launch_node_grad<__bf16, 128>(&edges[0], t, q0.dz0, q0.dx_part, q0.dP8, dx, st)) return r;
-    return wgrad(0);
-}
-
 }  // extern "C"

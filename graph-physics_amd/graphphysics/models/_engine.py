@@ -15,30 +15,12 @@ Device memory is always allocated here through the PyTorch caching allocator; th
 none. No CPU fallback exists: tensors must live on a HIP device.
 """
 import ctypes
-import os
 import weakref
 
 import torch
 import torch.nn as nn
 
 from graphphysics import _native as nat
-
-
-# processor-stack backward (mgn_processor_backward: each node-MLP backward also forms the next
-# block's data gradient) — opt-in (env MGN_PROCESSOR=1): measured on Cfg B it is no faster than the
-# per-block calls (271 vs 282 steps/s): both node-side kernels are single-tile latency chains, so
-# folding one into the other lengthens the chain by about what the separate launch cost
-USE_PROCESSOR = os.environ.get("MGN_PROCESSOR", "0") == "1"
-
-
-def _processor_ok(topo, edescs, ndescs):
-    nb = len(edescs)
-    if not USE_PROCESSOR or nb == 0:
-        return None
-    ea, na = (nat.Mlp * nb)(*edescs), (nat.Mlp * nb)(*ndescs)
-    if not nat.lib().mgn_processor_supported(ctypes.byref(topo.struct), nb, ea, na):
-        return None
-    return ea, na
 
 
 # --------------------------------------------------------------------------- topology
@@ -388,13 +370,7 @@ class EPDFunction(torch.autograd.Function):
             bdescs, boff = descs, off
         else:
             bdescs, boff = descs[3:], off[3:]
-        nb = len(bdescs) // 2
-        proc = _processor_ok(topo, [bdescs[2 * b] for b in range(nb)], [bdescs[2 * b + 1] for b in range(nb)])
         need = _ws_bytes_block(topo, bdescs[0], bdescs[1]) if len(bdescs) >= 2 else 0
-        if proc is not None:
-            need = int(nat.lib().mgn_processor_backward_workspace_bytes(ctypes.byref(topo.struct),
-                                                                        ctypes.byref(bdescs[0]),
-                                                                        ctypes.byref(bdescs[1])))
         if not ctx.only_processor:
             need = max(need, _ws_bytes_mlp(descs[0], N), _ws_bytes_mlp(descs[1], E),
                        _ws_bytes_mlp(descs[2], N))
@@ -406,26 +382,12 @@ class EPDFunction(torch.autograd.Function):
             g = gout.detach().float().contiguous()
             _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                      ctypes.c_void_p(gp + 4 * off[2]), ws, st)
+        nb = len(bdescs) // 2
         # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
         # gradient is zero, which the chained bf16 kernels take as NULL (no zero fill, no reads)
         de = None if nb and nat.lib().mgn_block_forward_inference_supported(
             ctypes.byref(bdescs[2 * nb - 2]), ctypes.byref(bdescs[2 * nb - 1])) else \
             torch.zeros((E, H), dtype=tdt, device=dev)
-        if proc is not None:
-            # the whole processor stack in one call (cross-block fusion); block inputs xs[0..nb-1]
-            dx1 = torch.empty((N, H), dtype=tdt, device=dev)
-            de1 = torch.empty((E, H), dtype=tdt, device=dev)
-            vp = ctypes.c_void_p
-            xa = (vp * nb)(*[xs[b].data_ptr() for b in range(nb)])
-            ea = (vp * nb)(*[es[b].data_ptr() for b in range(nb)])
-            sva = (nat.BlockSaved * nb)(*[svs[b][0] for b in range(nb)])
-            ega = (vp * nb)(*[gp + 4 * boff[2 * b] for b in range(nb)])
-            nga = (vp * nb)(*[gp + 4 * boff[2 * b + 1] for b in range(nb)])
-            nat.check(nat.lib().mgn_processor_backward(
-                ctypes.byref(topo.struct), nb, proc[0], proc[1], xa, ea, sva, nat.ptr(dx), nat.ptr(de),
-                nat.ptr(dx1), nat.ptr(de1), ega, nga, nat.ptr(ws), ws.numel(), st))
-            dx, de = dx1, de1
-            nb = 0  # done: skip the per-block loop
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
             de1 = torch.empty((E, H), dtype=tdt, device=dev)

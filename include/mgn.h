@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 5
+#define MGN_ABI_VERSION 4
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -165,28 +165,6 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
                        const void* dx_out, const void* de_out, void* dx, void* de,
                        float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                        mgn_stream_t stream);
-
-/* ---------------------------------------------------------------- processor stack */
-/* EncodeProcessDecode's processor loop (reference processors.py:130-131, backward of the nb
- * GraphNetBlock.forward calls layers.py:667-746): the same results as nb mgn_block_backward calls
- * (block nb-1 first, each block's dx/de feeding the previous one), but the library sees the whole
- * stack and fuses across blocks — block b's node-MLP backward kernel forms block b+1's data gradient
- * (its segment sums of dZ0 and the x blocks of its edge W0), so that step never runs as a separate
- * launch and dx never round-trips through HBM between blocks. Available where
- * mgn_processor_supported() is 1 (every block on the chained bf16 h = 128 kernels, E > 0, N > 0).
- * xs[b] / es[b]: the INPUTS of block b (as passed to its mgn_block_forward) and saved[b] its forward
- * state; dx_out / de_out: gradients w.r.t. the last block's outputs (de_out may be NULL: zero);
- * dx / de: receive the gradients w.r.t. xs[0] / es[0]; edge_grads[b] / node_grads[b]: as in
- * mgn_block_backward. All blocks share one shape. */
-int mgn_processor_supported(const mgn_topology* t, int32_t nb, const mgn_mlp* edges,
-                            const mgn_mlp* nodes);
-size_t mgn_processor_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
-                                              const mgn_mlp* node);
-int mgn_processor_backward(const mgn_topology* t, int32_t nb, const mgn_mlp* edges,
-                           const mgn_mlp* nodes, const void* const* xs, const void* const* es,
-                           const mgn_block_saved* saved, const void* dx_out, const void* de_out,
-                           void* dx, void* de, float* const* edge_grads, float* const* node_grads,
-                           void* ws, size_t ws_bytes, mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- primitives */
 /* out[k,:] = in[idx[k],:] (gather), or out[idx[k],:] = in[k,:] when scatter != 0. */

@@ -626,36 +626,3 @@ def test_encoder_mlp_bf16_chained_vs_fp64(rows, in_dim, gather, out_f32, din):
         assert relerr(gg, p64.grad) <= max(1e-2, 2 * relerr(pa.grad, p64.grad)), k
     if din:
         assert relerr(dind, x64.grad) <= max(1e-2, 2 * relerr(xac.grad, x64.grad))
-
-
-def test_processor_backward_matches_per_block():
-    """mgn_processor_backward (cross-block fusion: each node-MLP backward forms the next block's data
-    gradient) against the per-block mgn_block_backward calls on the same forward state, bf16 h=128
-    MP=4 on a CylinderFlow batch: input and parameter gradients within bf16 rounding of each other
-    (the per-block path rounds dx to bf16 between blocks, the fused path keeps it in fp32)."""
-    from graphphysics.models import _engine
-    from graphphysics.models.processors import EncodeProcessDecode
-    from graphphysics.utils import meshes
-    from graphphysics.utils.data import Data
-
-    b = meshes.cylinder_batch(2, jitter=0.01)
-    g = torch.Generator().manual_seed(11)
-    x = torch.randn(b["x"].shape[0], 11, generator=g).to(DEV)
-    ea = torch.randn(b["edge_attr"].shape[0], 3, generator=g).to(DEV)
-    ei = torch.from_numpy(b["edge_index"]).to(DEV)
-    gy = torch.randn(x.shape[0], 2, generator=g).to(DEV)
-    res = {}
-    old = _engine.USE_PROCESSOR
-    try:
-        for use in (False, True):
-            _engine.USE_PROCESSOR = use
-            torch.manual_seed(0)
-            m = EncodeProcessDecode(4, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
-            xd, ed = x.clone().requires_grad_(True), ea.clone().requires_grad_(True)
-            (m(Data(x=xd, edge_index=ei, edge_attr=ed)) * gy).sum().backward()
-            res[use] = dict(dx=xd.grad, de=ed.grad, **{k: p.grad for k, p in m.named_parameters()})
-    finally:
-        _engine.USE_PROCESSOR = old
-    for k, v in res[True].items():
-        assert torch.isfinite(v).all(), k
-        assert relerr(v, res[False][k]) < 2e-2, (k, relerr(v, res[False][k]))
