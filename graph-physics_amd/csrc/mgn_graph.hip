@@ -191,11 +191,11 @@ __global__ __launch_bounds__(256) void colstats_final(const float* __restrict__ 
 // _accumulate to the module's fp32 buffers exactly as the torch expressions do (acc += live ? s : 0,
 // live = num_acc < max_acc), and leaves mean / max(sqrt(max(var, 0)), eps) per column in mstd for
 // the elementwise pass.
-__global__ __launch_bounds__(256) void normalizer_update(const float* __restrict__ part, int nblocks, int cols,
-                                                        const float* __restrict__ pending, float rows_f,
-                                                        int accumulate, float* acc_sum, float* acc_sum_sq,
-                                                        float* acc_count, float* num_acc, float max_acc, float eps,
-                                                        float* __restrict__ mstd) {
+__device__ __forceinline__ void normalizer_update_body(const float* __restrict__ part, int nblocks, int cols,
+                                                       const float* __restrict__ pending, float rows_f,
+                                                       int accumulate, float* acc_sum, float* acc_sum_sq,
+                                                       float* acc_count, float* num_acc, float max_acc, float eps,
+                                                       float* __restrict__ mstd) {
 #pragma clang fp contract(off)  // one rounding per torch op: no fused multiply-adds here
     __shared__ float tot[2 * 32];
     const int i = threadIdx.x;
@@ -237,6 +237,98 @@ __global__ __launch_bounds__(256) void normalizer_update(const float* __restrict
         *acc_count = count_new;
         *num_acc = num_old + (live ? 1.f : 0.f);
     }
+}
+
+__global__ __launch_bounds__(256) void normalizer_update(const float* __restrict__ part, int nblocks, int cols,
+                                                        const float* __restrict__ pending, float rows_f,
+                                                        int accumulate, float* acc_sum, float* acc_sum_sq,
+                                                        float* acc_count, float* num_acc, float max_acc, float eps,
+                                                        float* __restrict__ mstd) {
+    normalizer_update_body(part, nblocks, cols, pending, rows_f, accumulate, acc_sum, acc_sum_sq, acc_count, num_acc,
+                           max_acc, eps, mstd);
+}
+
+// ----------------------------------------------------------------------- fused Simulator preamble
+// The three Normalizer.forward calls of Simulator._build_input_graph (simulator.py:206-290) on
+// "virtual" matrices read straight from x / y / edge_attr: source 0 = target delta y - x[:, os:oe],
+// source 1 = node features [x[:, fs:fe] ‖ one_hot(x[:, nti], n_types)], source 2 = edge_attr. Each
+// source's statistics use mgn_column_stats' partition and order, so every sum, buffer and output is
+// bit-identical to the unfused torch + mgn_normalizer_forward path; 3 launches instead of ~15.
+struct PreSrc {
+    const float* a;     // src 0: y, 1: x, 2: edge_attr
+    const float* b;     // src 0: x (pre-target), else unused
+    int64_t rows, lda, ldb;
+    int32_t cols, off_a, off_b, nf, nti, ntypes;  // src 1: nf feature columns at off_a, type column nti
+    int64_t rpb;        // rows per statistics block
+    int32_t nb, blk0;   // statistics blocks, first block index in the launch
+    float* part;        // [nb][2*cols]
+    float* mstd;        // [2*cols]
+    float* out;         // [rows][cols]
+    const float* pending;
+    float *acc_sum, *acc_sum_sq, *acc_count, *num_acc;
+    float max_acc, eps;
+};
+struct PreArgs {
+    PreSrc s[3];
+    int32_t nsrc, accumulate;
+    int64_t apply0[4];  // flat element offsets of the sources in the apply launch
+};
+
+__device__ __forceinline__ float pre_value(const PreSrc& q, int which, int64_t r, int c) {
+    if (which == 0) return q.a[r * q.lda + q.off_a + c] - q.b[r * q.ldb + q.off_b + c];
+    if (which == 1) {
+        if (c < q.nf) return q.a[r * q.lda + q.off_a + c];
+        const int64_t t = (int64_t)q.a[r * q.lda + q.nti];  // node_type.long() (truncation)
+        return t == (int64_t)(c - q.nf) ? 1.f : 0.f;
+    }
+    return q.a[r * q.lda + c];
+}
+
+__global__ __launch_bounds__(256) void preamble_stats(PreArgs a) {
+    __shared__ float red[256];
+    int w = 0;
+    while (w + 1 < a.nsrc && (int)blockIdx.x >= a.s[w + 1].blk0) ++w;
+    const PreSrc& q = a.s[w];
+    const int64_t b = (int64_t)blockIdx.x - q.blk0;
+    const int64_t r0 = b * q.rpb;
+    const int64_t r1 = r0 + q.rpb < q.rows ? r0 + q.rpb : q.rows;
+    for (int c = 0; c < q.cols; ++c) {  // colstats_partial's loop, on the virtual matrix
+        float s = 0.f, s2 = 0.f;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+            const float v = pre_value(q, w, r, c);
+            s += v;
+            s2 = fmaf(v, v, s2);
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            red[threadIdx.x] = pass ? s2 : s;
+            __syncthreads();
+            for (int k = 128; k > 0; k >>= 1) {
+                if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) q.part[b * 2 * q.cols + pass * q.cols + c] = red[0];
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void preamble_update(PreArgs a) {
+    const PreSrc& q = a.s[blockIdx.x];
+    normalizer_update_body(q.part, q.nb, q.cols, q.pending, (float)q.rows, a.accumulate, q.acc_sum, q.acc_sum_sq,
+                           q.acc_count, q.num_acc, q.max_acc, q.eps, q.mstd);
+}
+
+__global__ __launch_bounds__(256) void preamble_apply(PreArgs a) {
+#pragma clang fp contract(off)
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.apply0[a.nsrc]) return;
+    int w = 0;
+    while (w + 1 < a.nsrc && k >= a.apply0[w + 1]) ++w;
+    const PreSrc& q = a.s[w];
+    const int64_t i = k - a.apply0[w];
+    const int64_t r = i / q.cols;
+    const int c = (int)(i - r * q.cols);
+    q.out[i] = (pre_value(q, w, r, c) - q.mstd[c]) / q.mstd[q.cols + c];
 }
 
 __global__ __launch_bounds__(256) void normalizer_apply(const float* __restrict__ x, int64_t rows, int cols,
@@ -489,6 +581,79 @@ int mgn_normalizer_forward(const float* x, int64_t rows, int32_t cols, int64_t l
     if (rows * cols > 0) {
         hipLaunchKernelGGL(normalizer_apply, dim3((unsigned)cdiv64(rows * cols, 256)), dim3(256), 0, st, x, rows,
                            (int)cols, ld, (const float*)mstd, out);
+        MGN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+size_t mgn_simulator_preamble_workspace_bytes(int64_t num_nodes, int64_t num_edges) {
+    (void)num_nodes;
+    (void)num_edges;
+    return 3 * (256 + (size_t)STAT_BLOCKS * 2 * STAT_MAXC * sizeof(float));
+}
+
+int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
+                           int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end, const float* y,
+                           int64_t ldy, const float* edge_attr, int64_t E, int32_t edge_cols, int64_t lde,
+                           int32_t accumulate, const mgn_normalizer_state* out_norm,
+                           const mgn_normalizer_state* node_norm, const mgn_normalizer_state* edge_norm,
+                           float* target_out, float* node_out, float* edge_out, void* ws, size_t ws_bytes,
+                           mgn_stream_t stream) {
+    const int nf = feat_end - feat_start, no = out_end - out_start;
+    MGN_REQUIRE(x && y && out_norm && node_norm && target_out && node_out, "simulator preamble: NULL argument");
+    MGN_REQUIRE(nf >= 0 && n_types >= 1 && nf + n_types <= STAT_MAXC && no >= 1 && no <= STAT_MAXC,
+                "simulator preamble: node features and targets must have 1..32 columns");
+    MGN_REQUIRE(feat_end <= ldx && out_end <= ldx && type_index >= 0 && type_index < ldx && ldy >= no,
+                "simulator preamble: column ranges outside the rows");
+    MGN_REQUIRE(!edge_norm || (edge_attr && edge_out && edge_cols >= 1 && edge_cols <= STAT_MAXC && lde >= edge_cols),
+                "simulator preamble: edge normalizer needs edge_attr [E, 1..32]");
+    MGN_REQUIRE(ws_bytes >= mgn_simulator_preamble_workspace_bytes(N, E), "simulator preamble: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    PreArgs a;
+    memset(&a, 0, sizeof(a));
+    a.accumulate = accumulate;
+    const mgn_normalizer_state* ns[3] = {out_norm, node_norm, edge_norm};
+    a.nsrc = edge_norm ? 3 : 2;
+    char* w = reinterpret_cast<char*>(ws);
+    int blocks = 0;
+    int64_t flat = 0;
+    for (int i = 0; i < a.nsrc; ++i) {
+        PreSrc& q = a.s[i];
+        const mgn_normalizer_state* n = ns[i];
+        if (i == 0) {
+            q.a = y, q.b = x, q.rows = N, q.lda = ldy, q.ldb = ldx, q.cols = no, q.off_a = 0, q.off_b = out_start;
+            q.out = target_out;
+        } else if (i == 1) {
+            q.a = x, q.rows = N, q.lda = ldx, q.cols = nf + n_types, q.off_a = feat_start, q.nf = nf;
+            q.nti = type_index, q.ntypes = n_types, q.out = node_out;
+        } else {
+            q.a = edge_attr, q.rows = E, q.lda = lde, q.cols = edge_cols, q.out = edge_out;
+        }
+        q.mstd = reinterpret_cast<float*>(w + i * (256 + (size_t)STAT_BLOCKS * 2 * STAT_MAXC * sizeof(float)));
+        q.part = q.mstd + 64;
+        q.pending = n->pending;
+        q.acc_sum = n->acc_sum, q.acc_sum_sq = n->acc_sum_sq, q.acc_count = n->acc_count, q.num_acc = n->num_acc;
+        q.max_acc = n->max_acc, q.eps = n->eps;
+        q.blk0 = blocks;
+        if (accumulate && !n->pending && q.rows > 0) {  // mgn_column_stats' partition
+            q.rpb = cdiv64(q.rows, STAT_BLOCKS);
+            if (q.rpb < 256) q.rpb = 256;
+            q.nb = (int)cdiv64(q.rows, q.rpb);
+        }
+        blocks += q.nb;
+        a.apply0[i] = flat;
+        flat += q.rows * q.cols;
+    }
+    a.apply0[a.nsrc] = flat;
+    for (int i = a.nsrc + 1; i < 4; ++i) a.apply0[i] = flat;
+    if (blocks > 0) {
+        hipLaunchKernelGGL(preamble_stats, dim3(blocks), dim3(256), 0, st, a);
+        MGN_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(preamble_update, dim3(a.nsrc), dim3(256), 0, st, a);
+    MGN_LAUNCH_CHECK();
+    if (flat > 0) {
+        hipLaunchKernelGGL(preamble_apply, dim3((unsigned)cdiv64(flat, 256)), dim3(256), 0, st, a);
         MGN_LAUNCH_CHECK();
     }
     return 0;

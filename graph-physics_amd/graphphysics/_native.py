@@ -43,6 +43,11 @@ class BlockSaved(ctypes.Structure):
     _fields_ = [("edge", MlpSaved), ("node", MlpSaved), ("aggr", _vp)]
 
 
+class NormalizerState(ctypes.Structure):
+    _fields_ = [("acc_sum", _vp), ("acc_sum_sq", _vp), ("acc_count", _vp), ("num_acc", _vp), ("pending", _vp),
+                ("max_acc", _f32), ("eps", _f32)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("w", _vp), ("dst", _vp), ("dstT", _vp), ("n", _i32), ("k", _i32),
                 ("dtype", _i32), ("reserved", _i32)]
@@ -79,6 +84,11 @@ EXPORTS = {
     "mgn_normalizer_workspace_bytes": (_sz, [_i64, _i32]),
     "mgn_normalizer_forward": (_i32, [_vp, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp,
                                       _vp, _sz, _vp]),
+    "mgn_simulator_preamble_workspace_bytes": (_sz, [_i64, _i64]),
+    "mgn_simulator_preamble": (_i32, [_vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64,
+                                      _i32, _i64, _i32, ctypes.POINTER(NormalizerState),
+                                      ctypes.POINTER(NormalizerState), ctypes.POINTER(NormalizerState), _vp, _vp,
+                                      _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_workspace_bytes": (_sz, [_i64]),
     "mgn_masked_mse": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
@@ -195,6 +205,39 @@ def column_stats(x):
     check(lib().mgn_column_stats(ptr(x), rows, cols, x.stride(0), ptr(out), ptr(ws), ws.numel(),
                                  stream_ptr(x.device)))
     return out[:cols].view(1, cols), out[cols:].view(1, cols)
+
+
+def normalizer_state(n, accumulate):
+    """mgn_normalizer_state of a graphphysics Normalizer module (buffers updated in place)."""
+    pend = n._pending_packed if accumulate else None
+    return NormalizerState(n._acc_sum.data_ptr(), n._acc_sum_squared.data_ptr(), n._acc_count.data_ptr(),
+                           n._num_accumulations.data_ptr(), pend.data_ptr() if pend is not None else None,
+                           float(n._max_accumulations), n._eps())
+
+
+def simulator_preamble(x, y, edge_attr, feat, out, type_index, n_types, accumulate, out_norm, node_norm,
+                       edge_norm):
+    """Simulator._build_input_graph's three Normalizer.forward calls on libmgn
+    (mgn_simulator_preamble): returns (target_normalized [N, out], node_features_normalized
+    [N, nf + n_types], edge_attr_normalized [E, de] or None)."""
+    import torch
+
+    require_device(x)
+    N, E = x.shape[0], (edge_attr.shape[0] if edge_norm is not None else 0)
+    dev = x.device
+    to = torch.empty((N, out[1] - out[0]), dtype=torch.float32, device=dev)
+    no = torch.empty((N, feat[1] - feat[0] + n_types), dtype=torch.float32, device=dev)
+    eo = torch.empty((E, edge_attr.shape[1]), dtype=torch.float32, device=dev) if edge_norm is not None else None
+    ws = torch.empty(int(lib().mgn_simulator_preamble_workspace_bytes(N, E)), dtype=torch.uint8, device=dev)
+    acc = bool(accumulate)
+    st = [normalizer_state(n, acc) if n is not None else None for n in (out_norm, node_norm, edge_norm)]
+    check(lib().mgn_simulator_preamble(
+        ptr(x), N, x.stride(0), feat[0], feat[1], type_index, n_types, out[0], out[1], ptr(y), y.stride(0),
+        ptr(edge_attr) if eo is not None else None, E, edge_attr.shape[1] if eo is not None else 0,
+        edge_attr.stride(0) if eo is not None else 0, int(acc), ctypes.byref(st[0]), ctypes.byref(st[1]),
+        ctypes.byref(st[2]) if st[2] is not None else None, ptr(to), ptr(no), ptr(eo), ptr(ws), ws.numel(),
+        stream_ptr(dev)))
+    return to, no, eo
 
 
 def normalizer_forward(x, accumulate, pending, acc_sum, acc_sum_sq, acc_count, num_acc, max_acc, eps):

@@ -85,7 +85,33 @@ class Simulator(nn.Module):
         feats = inputs.x[:, self.feature_index_start:self.feature_index_end]
         return torch.cat([feats, one_hot_type], dim=1)
 
+    def _fused_preamble_ok(self, inputs, accumulate: bool) -> bool:
+        """The three Normalizer.forward calls run as one libmgn preamble (mgn_simulator_preamble)
+        when every input is a row-major fp32 HIP tensor and every normalizer takes its native path."""
+        if not os.environ.get("MGN_FUSED_PREAMBLE", "1") != "0":
+            return False
+        x, y, ea = inputs.x, getattr(inputs, "y", None), inputs.edge_attr
+        ts = [x, y] + ([ea] if self._edge_normalizer is not None else [])
+        if any(t is None or not t.is_cuda or t.dtype != torch.float32 or t.dim() != 2 or t.stride(1) != 1
+               or t.requires_grad for t in ts):
+            return False
+        if y.shape[0] != x.shape[0] or y.shape[1] < self.output_index_end - self.output_index_start:
+            return False
+        dummy = x[:1, :1]
+        return all(n._native_ok(dummy, accumulate) for n in self.normalizers())
+
     def _build_input_graph(self, inputs, is_training: bool) -> Tuple[Data, torch.Tensor]:
+        if self._fused_preamble_ok(inputs, is_training):
+            from graphphysics import _native as nat
+
+            tdn, nfn, ea = nat.simulator_preamble(
+                inputs.x, inputs.y, inputs.edge_attr, (self.feature_index_start, self.feature_index_end),
+                (self.output_index_start, self.output_index_end), self.node_type_index, NodeType.SIZE,
+                is_training, self._output_normalizer, self._node_normalizer, self._edge_normalizer)
+            if ea is None:
+                ea = inputs.edge_attr
+            graph = Data(x=nfn, pos=getattr(inputs, "pos", None), edge_attr=ea, edge_index=inputs.edge_index)
+            return graph, tdn
         tdn = self._get_target_normalized(inputs, is_training)
         nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
         nfn = self._node_normalizer(nf, is_training)

@@ -195,6 +195,32 @@ int mgn_normalizer_forward(const float* x, int64_t rows, int32_t cols, int64_t l
                            const float* pending, float* acc_sum, float* acc_sum_sq, float* acc_count, float* num_acc,
                            float max_acc, float eps, float* out, void* ws, size_t ws_bytes, mgn_stream_t stream);
 
+/* The Simulator's train/eval preamble (reference simulator.py:206-290, Simulator._build_input_graph):
+ * the three Normalizer.forward calls of mgn_normalizer_forward on
+ *   target delta   y[:, 0:oe-os] - x[:, os:oe]                          -> target_out [N, oe-os]
+ *   node features  [x[:, fs:fe] ‖ one_hot(long(x[:, type_index]), n_types)] -> node_out [N, fe-fs+n_types]
+ *   edge_attr      [E, edge_cols] (row stride lde; edge_norm NULL: none)  -> edge_out [E, edge_cols]
+ * read straight from x [N, ldx], y [N, ldy] and edge_attr (no intermediate tensors), in 3 launches.
+ * Statistics, buffers and outputs are bit-identical to the torch expressions + three
+ * mgn_normalizer_forward calls (same partition and order). A node type outside [0, n_types) gives an
+ * all-zero one-hot row (the reference's F.one_hot raises). Output columns <= 32 per normalizer. */
+typedef struct mgn_normalizer_state {
+    float* acc_sum;      /* [cols] */
+    float* acc_sum_sq;   /* [cols] */
+    float* acc_count;    /* scalar */
+    float* num_acc;      /* scalar */
+    const float* pending; /* NULL or float[2*cols + 1] {Σx, Σx², count} (see mgn_normalizer_forward) */
+    float max_acc, eps;
+} mgn_normalizer_state;
+size_t mgn_simulator_preamble_workspace_bytes(int64_t num_nodes, int64_t num_edges);
+int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
+                           int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end,
+                           const float* y, int64_t ldy, const float* edge_attr, int64_t E,
+                           int32_t edge_cols, int64_t lde, int32_t accumulate,
+                           const mgn_normalizer_state* out_norm, const mgn_normalizer_state* node_norm,
+                           const mgn_normalizer_state* edge_norm, float* target_out, float* node_out,
+                           float* edge_out, void* ws, size_t ws_bytes, mgn_stream_t stream);
+
 /* Masked L2 loss (reference utils/loss.py:10-65): *loss = Σ_r m_r Σ_c (pred - target)² / (count ·
  * cols) over row-major fp32 [rows, cols] pred/target, m_r = 1 when node_type[r·nt_ld] (a float
  * column, e.g. a strided view of x) is an integer t < 32 with bit t of type_mask set; count =

@@ -626,3 +626,45 @@ def test_encoder_mlp_bf16_chained_vs_fp64(rows, in_dim, gather, out_f32, din):
         assert relerr(gg, p64.grad) <= max(1e-2, 2 * relerr(pa.grad, p64.grad)), k
     if din:
         assert relerr(dind, x64.grad) <= max(1e-2, 2 * relerr(xac.grad, x64.grad))
+
+
+def test_fused_simulator_preamble_bitwise():
+    """mgn_simulator_preamble (target delta, one-hot node features and the three Normalizer.forward
+    calls from x / y / edge_attr in 3 launches) is bit-identical to the unfused path (torch feature
+    ops + mgn_normalizer_forward per normalizer): outputs and every normalizer buffer, over
+    accumulating steps, the max_accumulations cut-off, pending (exchanged) statistics and eval."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(3, jitter=0.01)
+    data = Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})
+    sims = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        s = Simulator(11, 3, 2, 0, 2, 0, 2, 2, EncodeProcessDecode(2, 11, 3, 2, 16), DEV)
+        for n in s.normalizers():
+            n._max_accumulations = 3
+        sims.append(s)
+    fused, plain = sims
+    plain._fused_preamble_ok = lambda inputs, acc: False
+    for it in range(6):
+        x = data.x.clone()
+        x[:, :2] *= 1 + 0.1 * it  # velocities only: the node-type column must stay a valid class
+        d = Data(x=x, y=data.y + 0.01 * it, edge_index=data.edge_index,
+                 edge_attr=data.edge_attr * (1 + 0.05 * it))
+        train = it != 4
+        if it == 5:  # statistics handed in, as the data-parallel prologue does
+            for s in sims:
+                s.exchange_statistics(d)
+        assert fused._fused_preamble_ok(d, train)
+        g1, t1 = fused._build_input_graph(d, train)
+        g2, t2 = plain._build_input_graph(d, train)
+        assert torch.equal(t1, t2) and torch.equal(g1.x, g2.x) and torch.equal(g1.edge_attr, g2.edge_attr), it
+        for n1, n2 in zip(fused.normalizers(), plain.normalizers()):
+            for name in ("_acc_sum", "_acc_sum_squared", "_acc_count", "_num_accumulations"):
+                assert torch.equal(getattr(n1, name), getattr(n2, name)), (it, n1.name, name)
+            n1.clear_pending()
+            n2.clear_pending()
+    assert float(fused._node_normalizer._num_accumulations) == 3.0
