@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 4
+#define MGN_ABI_VERSION 5
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
