@@ -318,6 +318,20 @@ __global__ __launch_bounds__(256) void preamble_update(PreArgs a) {
                            q.acc_count, q.num_acc, q.max_acc, q.eps, q.mstd);
 }
 
+// batch statistics only (the data-parallel prologue): per source {Σx, Σx², rows}, packed in source
+// order, with colstats_final's order over the partial rows
+__global__ __launch_bounds__(256) void preamble_stats_final(PreArgs a, float* __restrict__ packed) {
+    const PreSrc& q = a.s[blockIdx.x];
+    int64_t off = 0;
+    for (int i = 0; i < (int)blockIdx.x; ++i) off += 2 * a.s[i].cols + 1;
+    const int lane = threadIdx.x & 63;
+    for (int o = threadIdx.x >> 6; o < 2 * q.cols; o += 4) {
+        const float t = partial_total(q.part, q.nb, q.cols, o, lane);
+        if (lane == 0) packed[off + o] = t;
+    }
+    if (threadIdx.x == 0) packed[off + 2 * q.cols] = (float)q.rows;
+}
+
 __global__ __launch_bounds__(256) void preamble_apply(PreArgs a) {
 #pragma clang fp contract(off)
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -590,6 +604,53 @@ size_t mgn_simulator_preamble_workspace_bytes(int64_t num_nodes, int64_t num_edg
     (void)num_nodes;
     (void)num_edges;
     return 3 * (256 + (size_t)STAT_BLOCKS * 2 * STAT_MAXC * sizeof(float));
+}
+
+int mgn_simulator_statistics(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
+                             int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end, const float* y,
+                             int64_t ldy, const float* edge_attr, int64_t E, int32_t edge_cols, int64_t lde,
+                             float* packed, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    const int nf = feat_end - feat_start, no = out_end - out_start;
+    MGN_REQUIRE(x && y && packed, "simulator statistics: NULL argument");
+    MGN_REQUIRE(nf >= 0 && n_types >= 1 && nf + n_types <= STAT_MAXC && no >= 1 && no <= STAT_MAXC,
+                "simulator statistics: node features and targets must have 1..32 columns");
+    MGN_REQUIRE(feat_end <= ldx && out_end <= ldx && type_index >= 0 && type_index < ldx && ldy >= no,
+                "simulator statistics: column ranges outside the rows");
+    MGN_REQUIRE(!edge_attr || (edge_cols >= 1 && edge_cols <= STAT_MAXC && lde >= edge_cols),
+                "simulator statistics: edge_attr must be [E, 1..32]");
+    MGN_REQUIRE(ws_bytes >= mgn_simulator_preamble_workspace_bytes(N, E), "simulator statistics: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    PreArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nsrc = edge_attr ? 3 : 2;
+    char* w = reinterpret_cast<char*>(ws);
+    int blocks = 0;
+    for (int i = 0; i < a.nsrc; ++i) {
+        PreSrc& q = a.s[i];
+        if (i == 0) {
+            q.a = y, q.b = x, q.rows = N, q.lda = ldy, q.ldb = ldx, q.cols = no, q.off_b = out_start;
+        } else if (i == 1) {
+            q.a = x, q.rows = N, q.lda = ldx, q.cols = nf + n_types, q.off_a = feat_start, q.nf = nf;
+            q.nti = type_index, q.ntypes = n_types;
+        } else {
+            q.a = edge_attr, q.rows = E, q.lda = lde, q.cols = edge_cols;
+        }
+        q.part = reinterpret_cast<float*>(w + i * (256 + (size_t)STAT_BLOCKS * 2 * STAT_MAXC * sizeof(float))) + 64;
+        q.blk0 = blocks;
+        if (q.rows > 0) {  // mgn_column_stats' partition
+            q.rpb = cdiv64(q.rows, STAT_BLOCKS);
+            if (q.rpb < 256) q.rpb = 256;
+            q.nb = (int)cdiv64(q.rows, q.rpb);
+        }
+        blocks += q.nb;
+    }
+    if (blocks > 0) {
+        hipLaunchKernelGGL(preamble_stats, dim3(blocks), dim3(256), 0, st, a);
+        MGN_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(preamble_stats_final, dim3(a.nsrc), dim3(256), 0, st, a, packed);
+    MGN_LAUNCH_CHECK();
+    return 0;
 }
 
 int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,

@@ -89,6 +89,8 @@ EXPORTS = {
                                       _i32, _i64, _i32, ctypes.POINTER(NormalizerState),
                                       ctypes.POINTER(NormalizerState), ctypes.POINTER(NormalizerState), _vp, _vp,
                                       _vp, _vp, _sz, _vp]),
+    "mgn_simulator_statistics": (_i32, [_vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64,
+                                        _i32, _i64, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_workspace_bytes": (_sz, [_i64]),
     "mgn_masked_mse": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
@@ -238,6 +240,23 @@ def simulator_preamble(x, y, edge_attr, feat, out, type_index, n_types, accumula
         ctypes.byref(st[2]) if st[2] is not None else None, ptr(to), ptr(no), ptr(eo), ptr(ws), ws.numel(),
         stream_ptr(dev)))
     return to, no, eo
+
+
+def simulator_statistics(x, y, edge_attr, feat, out, type_index, n_types, packed):
+    """Batch statistics of the Simulator's three normalizers into `packed` (mgn_simulator_statistics);
+    edge_attr None: two normalizers."""
+    import torch
+
+    require_device(x)
+    N = x.shape[0]
+    E = edge_attr.shape[0] if edge_attr is not None else 0
+    ws = torch.empty(int(lib().mgn_simulator_preamble_workspace_bytes(N, E)), dtype=torch.uint8, device=x.device)
+    check(lib().mgn_simulator_statistics(
+        ptr(x), N, x.stride(0), feat[0], feat[1], type_index, n_types, out[0], out[1], ptr(y), y.stride(0),
+        ptr(edge_attr), E, edge_attr.shape[1] if edge_attr is not None else 0,
+        edge_attr.stride(0) if edge_attr is not None else 0, ptr(packed), ptr(ws), ws.numel(),
+        stream_ptr(x.device)))
+    return packed
 
 
 def normalizer_forward(x, accumulate, pending, acc_sum, acc_sum_sq, acc_count, num_acc, max_acc, eps):

@@ -105,6 +105,14 @@ class Normalizer(nn.Module):
         self._pending[1].copy_(s2)
         self._pending[2].copy_(cnt.reshape(()))
 
+    def bind_pending(self, packed_view: torch.Tensor):
+        """Keep the pending statistics in `packed_view` (float32 [2*size + 1], e.g. a slice of one
+        buffer several normalizers share so that a single all-reduce updates them all in place)."""
+        k = self._acc_sum.numel()
+        self._pending_packed = packed_view
+        self._pending = (packed_view[:k].view_as(self._acc_sum), packed_view[k:2 * k].view_as(self._acc_sum_squared),
+                         packed_view[2 * k])
+
     def clear_pending(self):
         self._pending = None
         self._pending_packed = None

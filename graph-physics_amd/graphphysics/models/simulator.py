@@ -55,6 +55,30 @@ class Simulator(nn.Module):
         exchanging them before the (captured) forward is exact."""
         import torch.distributed as dist
 
+        if self._fused_preamble_ok(inputs, False):
+            # one libmgn pass writes every normalizer's {Σx, Σx², count} into one buffer the
+            # normalizers' pending statistics are views of: one all-reduce, no copies
+            from graphphysics import _native as nat
+
+            norms = self.normalizers()
+            sizes = [2 * n._acc_sum.numel() + 1 for n in norms]
+            buf = getattr(self, "_stats_buf", None)
+            if buf is None or buf.numel() != sum(sizes) or buf.device != inputs.x.device or \
+                    any(n._pending_packed is None for n in norms):
+                buf = torch.zeros(sum(sizes), dtype=torch.float32, device=inputs.x.device)
+                o = 0
+                for n, k in zip(norms, sizes):
+                    n.bind_pending(buf[o:o + k])
+                    o += k
+                self._stats_buf = buf
+            nat.simulator_statistics(inputs.x, inputs.y,
+                                     inputs.edge_attr if self._edge_normalizer is not None else None,
+                                     (self.feature_index_start, self.feature_index_end),
+                                     (self.output_index_start, self.output_index_end), self.node_type_index,
+                                     NodeType.SIZE, buf)
+            if dist.is_available() and dist.is_initialized():
+                dist.all_reduce(buf, group=group)
+            return
         delta = inputs.y - self._get_pre_target(inputs)
         nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
         srcs = [(self._output_normalizer, delta), (self._node_normalizer, nf)]

@@ -46,7 +46,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 5
+#define MGN_ABI_VERSION 6
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -220,6 +220,17 @@ int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_
                            const mgn_normalizer_state* out_norm, const mgn_normalizer_state* node_norm,
                            const mgn_normalizer_state* edge_norm, float* target_out, float* node_out,
                            float* edge_out, void* ws, size_t ws_bytes, mgn_stream_t stream);
+
+/* The batch statistics of the same three normalizers without updating them (the data-parallel
+ * prologue: summed over ranks, then handed to mgn_simulator_preamble as `pending`): packed =
+ * [Σ target delta, Σ target delta², N, Σ node features, Σ node features², N, (Σ edge_attr,
+ * Σ edge_attr², E if edge_attr != NULL)] — each block the float[2*cols + 1] layout of `pending`, with
+ * the same sums as mgn_column_stats. Workspace: mgn_simulator_preamble_workspace_bytes. */
+int mgn_simulator_statistics(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
+                             int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end,
+                             const float* y, int64_t ldy, const float* edge_attr, int64_t E,
+                             int32_t edge_cols, int64_t lde, float* packed, void* ws, size_t ws_bytes,
+                             mgn_stream_t stream);
 
 /* Masked L2 loss (reference utils/loss.py:10-65): *loss = Σ_r m_r Σ_c (pred - target)² / (count ·
  * cols) over row-major fp32 [rows, cols] pred/target, m_r = 1 when node_type[r·nt_ld] (a float
