@@ -20,7 +20,7 @@
 #include "mgn_chain.h"
 
 #ifndef MGN_NODE_AG
-#define MGN_NODE_AG 8  // in-edges gathered per round trip by the node-MLP aggregation
+#define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
 #endif
 
 namespace {
@@ -765,6 +765,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
             if (l == 0)
                 gemm16_layer0(acc, W, xb, Ba, a.wpack + a.woff[0],
                               [](int t, int s) { return t * 8 + 4 + s; }, lane);
+            else if (SAVE)  // stores its input (the R8 save of layer l) under the MFMAs
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
             else
                 gemm16(acc, W, l, B, lane);
             unsigned bits = 0u;
@@ -779,12 +781,12 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                 }
             }
             to_operand(acc, B);
-            if (SAVE) {
-                a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
-                store_r8(acc, scr, a.act8 + a.act_off[l + 1], tile, lane);
-            }
+            if (SAVE) a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
         }
-        gemm16(acc, W, 3, B, lane);
+        if (SAVE)
+            gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+        else
+            gemm16(acc, W, 3, B, lane);
         STAMP(2);
         float ss = 0.f;
 #pragma unroll
@@ -885,16 +887,15 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         STAMP(1);
         bf16x8 B[4];
         to_operand(acc, B);
-        store_r8(acc, scr, a.dz8 + 3 * a.RP * H, tile, lane);
+        // each GEMM stores its B operand dZ_l (R8) under its MFMAs
 #pragma unroll
         for (int l = 3; l >= 1; --l) {
-            gemm16(acc, W, l, B, lane);
+            gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
             relu_mask(acc, mk[l - 1]);
             to_operand(acc, B);
-            store_r8(acc, scr, a.dz8 + (int64_t)(l - 1) * a.RP * H, tile, lane);
         }
         // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
-        gemm16(acc, W, 0, B, lane);
+        gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, nullptr}, tile, a.M);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
         store_rows(acc, scr, a.dx_part, tile, a.M, lane);
