@@ -39,6 +39,12 @@ constexpr size_t LDS_V = (size_t)6 * H * 4;             // 4 bias vectors + scal
 constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose scratch
 constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
 constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
+// edge kernels, per waves-per-workgroup NWK (8: two waves per SIMD; 12: three): forward = weights |
+// bias[4] + scale | scratch, backward = weights | scale | scratch | dscale partials (12 waves: 160 KiB)
+constexpr size_t LDS_VF = (size_t)5 * H * 4, LDS_VB = (size_t)H * 4;
+constexpr size_t lds_fwd(int nwk) { return LDS_W + LDS_VF + (size_t)nwk * SROWS * SLD * 2; }
+constexpr size_t lds_bwd(int nwk) { return LDS_W + LDS_VB + (size_t)nwk * SROWS * SLD * 2 + (size_t)nwk * H * 4; }
+static_assert(lds_bwd(12) <= 163840, "12-wave edge backward exceeds 160 KiB of LDS");
 
 // Diagnostics (build with -DMGN_STAMPS, e.g. MGN_STAMPS=1 python __graft_entry__.py): per-phase
 // s_memtime deltas of wave 0 of workgroup 0, printed once per launch. Not in normal builds.
@@ -126,14 +132,15 @@ __device__ __forceinline__ void relu_mask(f4 (&acc)[8], unsigned w) {
 // (A = W forward, Wᵀ backward). Linear walk over libmgn's 16x16x32 packs (16-byte coalesced loads):
 // a source chunk holds 8 consecutive reduction indices 32s + 8q .. +7 of one row; its halves go to
 // lane groups g = 2(q&1) + half, element group jg = q>>1.
-template <int NL = 4>
+template <int NL = 4, int NT = NW * 64>
 __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
                                         bool transposed) {
-    constexpr int PER = NL * 2048 / (NW * 64);  // 16 chunks per thread (4 layers)
+    constexpr int TOT = NL * 2048, PER = (TOT + NT - 1) / NT;  // 16 chunks per thread (4 layers, 512 threads)
     u32x4 v[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int it = threadIdx.x + u * NW * 64;
+        const int it = threadIdx.x + u * NT;
+        if (TOT % NT != 0 && it >= TOT) break;
         const int l = it >> 11, c = it & 2047;
         const int tile = c >> 6, lane16 = c & 63;
         const int rt = tile >> 2, ks = tile & 3;
@@ -142,7 +149,8 @@ __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int it = threadIdx.x + u * NW * 64;
+        const int it = threadIdx.x + u * NT;
+        if (TOT % NT != 0 && it >= TOT) break;
         const int l = it >> 11, c = it & 2047;
         const int tile = c >> 6, lane16 = c & 63;
         const int rt = tile >> 2, ks = tile & 3;
@@ -313,10 +321,26 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
     }
 }
 
-int chain16_grid(int64_t ntiles) {
+int chain16_grid(int64_t ntiles, int nwk = NW) {
     const int cus = device_cus();
-    const int64_t groups = cdiv64(ntiles, NW);
+    const int64_t groups = cdiv64(ntiles, nwk);
     return (int)(groups < cus ? groups : cus);
+}
+
+// waves per workgroup of the edge kernels, read once per process. Forward: 12 (three per SIMD; Cfg B
+// 40.9 vs 42.5 us at 8); backward: 8 (at 12 its 168-VGPR cap spills 17 registers: 54.7 vs 50.6 us).
+// env MGN_EDGE_WAVES / MGN_EDGE_BWD_WAVES = 8 or 12 override, for A/B
+static int waves_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && (atoi(e) == 8 || atoi(e) == 12) ? atoi(e) : dflt;
+}
+int edge_waves() {
+    static const int v = waves_env("MGN_EDGE_WAVES", 12);
+    return v;
+}
+int edge_bwd_waves() {
+    static const int v = waves_env("MGN_EDGE_BWD_WAVES", 8);
+    return v;
 }
 
 void layer_offsets(const mgn_mlp* m, int64_t* woff, int* wks) {
@@ -355,24 +379,24 @@ __device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, in
 
 // SAVE = false: inference (no autograd): only z and rden (the node MLP's aggregation inputs) are
 // written — no R8 layer inputs, no ReLU masks (≈ 40 % of the training forward's HBM bytes)
-template <bool SAVE>
-__global__ __launch_bounds__(NW * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
+template <bool SAVE, int NWK>
+__global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
     float* vec = reinterpret_cast<float*>(smem + LDS_W);  // bias[4][H], scale[H]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_VF) + wave * SROWS * SLD;
     const int m = lane & 15, g = lane >> 4;
-    const int64_t stride = (int64_t)gridDim.x * NW;
-    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t stride = (int64_t)gridDim.x * NWK;
+    int64_t tile = (int64_t)blockIdx.x * NWK + wave;
     const int64_t last = a.ntiles - 1;
     STAMP_DECL;
     In16 nxt;
     int di, dj;
     load_idx(a, min(tile, last), lane, di, dj);
     load_e(nxt, a, min(tile, last), lane);
-    stage16(W, a.wpack, a.woff, a.wks, false);
-    for (int i = threadIdx.x; i < 5 * H; i += NW * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
+    stage16<4, NWK * 64>(W, a.wpack, a.woff, a.wks, false);
+    for (int i = threadIdx.x; i < 5 * H; i += NWK * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
     __syncthreads();
     if (tile >= a.ntiles) return;
 #pragma unroll
@@ -513,25 +537,25 @@ __device__ __forceinline__ void pin_in(const S& in) {
     for (int l = 0; l < 3; ++l) pin(in.mask[l]);
 }
 
-template <bool ZD>
-__global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
+template <bool ZD, int NWK>
+__global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
     float* vec = reinterpret_cast<float*>(smem + LDS_W);  // scale[H]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_V) + wave * SROWS * SLD;
-    float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
+    __bf16* scr = reinterpret_cast<__bf16*>(smem + LDS_W + LDS_VB) + wave * SROWS * SLD;
+    float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_VB + (size_t)NWK * SROWS * SLD * 2);  // [NWK][H]
     const int m = lane & 15, g = lane >> 4;
     const int r4 = 2 * (m & 1) + ((m >> 1) & 1);  // row16_sum4's component in lane m
-    const int64_t stride = (int64_t)gridDim.x * NW;
-    int64_t tile = (int64_t)blockIdx.x * NW + wave;
+    const int64_t stride = (int64_t)gridDim.x * NWK;
+    int64_t tile = (int64_t)blockIdx.x * NWK + wave;
     const int64_t last = a.ntiles - 1;
     STAMP_DECL;
     const int gi0 = bidx(a, min(tile, last), lane);
-    stage16(W, a.wtpack, a.woff, a.wks, true);
+    stage16<4, NWK * 64>(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
     bload<ZD>(nxt, a, min(tile, last), gi0, lane);
-    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
+    for (int i = threadIdx.x; i < H; i += NWK * 64) vec[i] = a.scale[i];
     __syncthreads();
     // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
     // over the tile's 16 edges, then the 4 lane-group leaders add their features; fixed order)
@@ -626,7 +650,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     if (threadIdx.x < H) {
         float s = 0.f;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) s += red[w * H + threadIdx.x];
+        for (int w = 0; w < NWK; ++w) s += red[w * H + threadIdx.x];
         a.dscale_part[(int64_t)blockIdx.x * H + threadIdx.x] = s;
     }
 }
@@ -1248,7 +1272,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_dense_bwd_kernel(ChainDenseBw
 
 int set_lds_once(const void* fn, size_t bytes) {
     static std::mutex mu;
-    static const void* done[16] = {};
+    static const void* done[32] = {};
     std::lock_guard<std::mutex> lk(mu);
     for (const void* d : done)
         if (d == fn) return 0;
@@ -1286,10 +1310,13 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, con
     a.mask32 = reinterpret_cast<unsigned*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     if (a.ntiles == 0) return 0;
-    const auto kern = sv->act ? chain16_fwd_kernel<true> : chain16_fwd_kernel<false>;
-    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
+    const int nwk = edge_waves();
+    const auto kern = nwk == 12 ? (sv->act ? chain16_fwd_kernel<true, 12> : chain16_fwd_kernel<false, 12>)
+                                : (sv->act ? chain16_fwd_kernel<true, 8> : chain16_fwd_kernel<false, 8>);
+    const size_t lds = lds_fwd(nwk);
+    if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
     ProfScope ps(PROF_FWD_EDGE, st);
-    hipLaunchKernelGGL(kern, dim3(chain16_grid(a.ntiles)), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(kern, dim3(chain16_grid(a.ntiles, nwk)), dim3(nwk * 64), lds, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }
@@ -1319,12 +1346,15 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.dz0 = reinterpret_cast<__bf16*>(dz0);
     *nparts = 0;
     if (a.ntiles == 0) return 0;
-    const auto kern = dout ? chain16_bwd_kernel<false> : chain16_bwd_kernel<true>;
-    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
-    const int grid = chain16_grid(a.ntiles);
+    const int nwk = edge_bwd_waves();
+    const auto kern = nwk == 12 ? (dout ? chain16_bwd_kernel<false, 12> : chain16_bwd_kernel<true, 12>)
+                                : (dout ? chain16_bwd_kernel<false, 8> : chain16_bwd_kernel<true, 8>);
+    const size_t lds = lds_bwd(nwk);
+    if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
+    const int grid = chain16_grid(a.ntiles, nwk);
     *nparts = grid;
     ProfScope ps(PROF_BWD_EDGE, st);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nwk * 64), lds, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }
