@@ -327,8 +327,9 @@ int chain16_grid(int64_t ntiles, int nwk = NW) {
     return (int)(groups < cus ? groups : cus);
 }
 
-// waves per workgroup of the edge kernels, read once per process. Forward: 12 (three per SIMD; Cfg B
-// 40.9 vs 42.5 us at 8); backward: 8 (at 12 its 168-VGPR cap spills 17 registers: 54.7 vs 50.6 us).
+// waves per workgroup of the edge kernels, read once per process: 12 (three per SIMD) for both. Cfg B:
+// forward 40.9 vs 42.5 us at 8; backward 47.9 vs 50.6 us, with its d_aggr gather loaded by the tile
+// instead of prefetched (prefetched, the 168-VGPR cap spills 17 registers: 54.7 us).
 // env MGN_EDGE_WAVES / MGN_EDGE_BWD_WAVES = 8 or 12 override, for A/B
 static int waves_env(const char* name, int dflt) {
     const char* e = getenv(name);
@@ -339,7 +340,7 @@ int edge_waves() {
     return v;
 }
 int edge_bwd_waves() {
-    static const int v = waves_env("MGN_EDGE_BWD_WAVES", 8);
+    static const int v = waves_env("MGN_EDGE_BWD_WAVES", 12);
     return v;
 }
 
@@ -502,7 +503,8 @@ struct BIn16 {  // raw bf16: features 16t + 4g .. +3
 };
 
 // ZD: de_out is identically zero (the processor's last block: EncodeProcessDecode returns nodes only)
-template <bool ZD>
+// PGA: prefetch the d_aggr gather with the rest (false: the tile loads it itself, 16 VGPRs fewer)
+template <bool ZD, bool PGA = true>
 __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
     const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
     const int off = 4 * (lane >> 4);
@@ -512,7 +514,7 @@ __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t 
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         in.d[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
-        in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+        if (PGA) in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
         in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
     }
     in.q = a.rden_save[row];
@@ -524,12 +526,12 @@ __device__ __forceinline__ int bidx(const ChainBwdArgs& a, int64_t tile, int lan
     return a.gath_idx[clamp_row(tile * TR + (lane & 15), a.M)];
 }
 
-template <class S>
+template <bool PGA = true, class S>
 __device__ __forceinline__ void pin_in(const S& in) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         pin(in.d[t]);
-        pin(in.ga[t]);
+        if (PGA) pin(in.ga[t]);
         pin(in.z[t]);
     }
     pin(in.q);
@@ -551,10 +553,12 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     int64_t tile = (int64_t)blockIdx.x * NWK + wave;
     const int64_t last = a.ntiles - 1;
     STAMP_DECL;
+    constexpr bool PGA = NWK < 12;  // three waves per SIMD: the gather is not prefetched (VGPR cap)
     const int gi0 = bidx(a, min(tile, last), lane);
+    int gcur = gi0;
     stage16<4, NWK * 64>(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
-    bload<ZD>(nxt, a, min(tile, last), gi0, lane);
+    bload<ZD, PGA>(nxt, a, min(tile, last), gi0, lane);
     for (int i = threadIdx.x; i < H; i += NWK * 64) vec[i] = a.scale[i];
     __syncthreads();
     // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
@@ -563,7 +567,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     int ngi = 0;
     if (tile < a.ntiles) {
         ngi = bidx(a, min(tile + stride, last), lane);
-        pin_in(nxt);
+        pin_in<PGA>(nxt);
         pin(ngi);
     }
     STAMP(0);
@@ -573,9 +577,15 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         // RMSNorm backward (layers.py:59-74) from the prefetched tile
         f4 acc[8];
         float dot = 0.f;
+        u32x2 gac[8];
+        if constexpr (!PGA) {
+            const __bf16* gp = a.gath + (int64_t)gcur * H + 4 * g;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+        }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-            const f4 dy = bf4(nxt.d[t]) + bf4(nxt.ga[t]);
+            const f4 dy = bf4(nxt.d[t]) + bf4(PGA ? nxt.ga[t] : gac[t]);
             const f4 z = bf4(nxt.z[t]);
             const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
             acc[t] = dy;
@@ -609,7 +619,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
         for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
         STAMP(1);
-        bload<ZD>(nxt, a, min(tile + stride, last), ngi, lane);
+        bload<ZD, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
         bf16x8 B[4];
         to_operand(acc, B);
@@ -639,8 +649,9 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             if (!ZD) acc[t] += bf4(dre[t]);
         store_rows(acc, scr, a.de, tile, a.M, lane);
         STAMP(7);
-        pin_in(nxt);
+        pin_in<PGA>(nxt);
         pin(ngi2);
+        gcur = ngi;
         ngi = ngi2;
         STAMP(8);
     }
