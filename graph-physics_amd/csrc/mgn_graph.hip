@@ -285,31 +285,33 @@ __device__ __forceinline__ float pre_value(const PreSrc& q, int which, int64_t r
 }
 
 __global__ __launch_bounds__(256) void preamble_stats(PreArgs a) {
-    __shared__ float red[256];
+    // colstats_partial's per-column arithmetic and tree order, all columns' trees advanced together
+    // (one barrier per level instead of two trees per column)
+    __shared__ float red[2 * STAT_MAXC][256];
     int w = 0;
     while (w + 1 < a.nsrc && (int)blockIdx.x >= a.s[w + 1].blk0) ++w;
     const PreSrc& q = a.s[w];
     const int64_t b = (int64_t)blockIdx.x - q.blk0;
     const int64_t r0 = b * q.rpb;
     const int64_t r1 = r0 + q.rpb < q.rows ? r0 + q.rpb : q.rows;
-    for (int c = 0; c < q.cols; ++c) {  // colstats_partial's loop, on the virtual matrix
+    const int cols = q.cols;
+    for (int c = 0; c < cols; ++c) {
         float s = 0.f, s2 = 0.f;
         for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
             const float v = pre_value(q, w, r, c);
             s += v;
             s2 = fmaf(v, v, s2);
         }
-        for (int pass = 0; pass < 2; ++pass) {
-            red[threadIdx.x] = pass ? s2 : s;
-            __syncthreads();
-            for (int k = 128; k > 0; k >>= 1) {
-                if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-                __syncthreads();
-            }
-            if (threadIdx.x == 0) q.part[b * 2 * q.cols + pass * q.cols + c] = red[0];
-            __syncthreads();
-        }
+        red[c][threadIdx.x] = s;
+        red[cols + c][threadIdx.x] = s2;
     }
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k)
+            for (int c = 0; c < 2 * cols; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x < 2 * cols) q.part[b * 2 * cols + threadIdx.x] = red[threadIdx.x][0];
 }
 
 __global__ __launch_bounds__(256) void preamble_update(PreArgs a) {
