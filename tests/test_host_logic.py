@@ -113,6 +113,8 @@ def test_simulator_preamble_matches_reference():
     ei, ea = torch.from_numpy(b["edge_index"]), torch.from_numpy(b["edge_attr"])
     sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _ZeroModel(), "cpu")
     ref = O.OracleSimulator(lambda xn, e_, ean: torch.zeros(xn.shape[0], 2), 11, 3, 2)
+    # host tensors never take the fused libmgn preamble (mgn_simulator_preamble needs HIP tensors)
+    assert not sim._fused_preamble_ok(Data(x=x, y=y, edge_index=ei, edge_attr=ea), True)
     for _ in range(2):
         _, tdn, _ = sim(Data(x=x, y=y, edge_index=ei, edge_attr=ea))
         _, tdn_r, _ = ref.forward(x, y, ei, ea, True)
