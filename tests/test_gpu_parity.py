@@ -628,7 +628,8 @@ def test_encoder_mlp_bf16_chained_vs_fp64(rows, in_dim, gather, out_f32, din):
         assert relerr(dind, x64.grad) <= max(1e-2, 2 * relerr(xac.grad, x64.grad))
 
 
-def test_fused_simulator_preamble_bitwise():
+@pytest.mark.parametrize("edge_norm", [True, False])
+def test_fused_simulator_preamble_bitwise(edge_norm):
     """mgn_simulator_preamble (target delta, one-hot node features and the three Normalizer.forward
     calls from x / y / edge_attr in 3 launches) is bit-identical to the unfused path (torch feature
     ops + mgn_normalizer_forward per normalizer): outputs and every normalizer buffer, over
@@ -643,7 +644,7 @@ def test_fused_simulator_preamble_bitwise():
     sims = []
     for _ in range(2):
         torch.manual_seed(0)
-        s = Simulator(11, 3, 2, 0, 2, 0, 2, 2, EncodeProcessDecode(2, 11, 3, 2, 16), DEV)
+        s = Simulator(11, 3 if edge_norm else 0, 2, 0, 2, 0, 2, 2, EncodeProcessDecode(2, 11, 3, 2, 16), DEV)
         for n in s.normalizers():
             n._max_accumulations = 3
         sims.append(s)
