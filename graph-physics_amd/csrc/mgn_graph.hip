@@ -117,17 +117,35 @@ __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, c
     const float decay = (float)(1.0 - lr * wd), w1 = (float)(1.0 - beta1), b2 = (float)beta2;
     const float omb2 = (float)(1.0 - beta2), bc2s = (float)sqrt(bc2), epsf = (float)eps;
     const float neg_step = (float)(-(lr / bc1));
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float pi = p[i] * decay;
-        const float gi = g[i];
-        float mi = fmaf(w1, gi - m[i], m[i]);
-        float vi = v[i] * b2;
+    auto upd = [&](float& pi, float gi, float& mi, float& vi) {
+        pi = pi * decay;
+        mi = fmaf(w1, gi - mi, mi);
+        vi = vi * b2;
         vi = vi + (omb2 * gi) * gi;
         const float den = sqrtf(vi) / bc2s + epsf;
         pi = pi + neg_step * (mi / den);
-        p[i] = pi;
-        m[i] = mi;
-        v[i] = vi;
+    };
+    // 16-byte vectors, several per thread: the double-precision schedule setup above is per thread,
+    // so each thread amortises it over many elements (scalar loop when a buffer is not 16-byte aligned)
+    const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+    const int64_t n4 = vec ? n / 4 : 0, stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < n4; i += stride) {
+        f4 P = reinterpret_cast<f4*>(p)[i], M = reinterpret_cast<f4*>(m)[i], V = reinterpret_cast<f4*>(v)[i];
+        const f4 G = reinterpret_cast<const f4*>(g)[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float pi = P[r], mi = M[r], vi = V[r];
+            upd(pi, G[r], mi, vi);
+            P[r] = pi, M[r] = mi, V[r] = vi;
+        }
+        reinterpret_cast<f4*>(p)[i] = P;
+        reinterpret_cast<f4*>(m)[i] = M;
+        reinterpret_cast<f4*>(v)[i] = V;
+    }
+    for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
+        float pi = p[i], mi = m[i], vi = v[i];
+        upd(pi, g[i], mi, vi);
+        p[i] = pi, m[i] = mi, v[i] = vi;
     }
 }
 
@@ -441,8 +459,8 @@ int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_av
                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
                   mgn_stream_t stream) {
     if (n == 0) return 0;
-    int64_t blocks = cdiv64(n, 256);
-    if (blocks > 4096) blocks = 4096;
+    int64_t blocks = cdiv64(cdiv64(n, 4), 256);
+    if (blocks > 512) blocks = 512;
     ProfScope ps(PROF_ADAMW, (hipStream_t)stream);
     hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
                        exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay);
