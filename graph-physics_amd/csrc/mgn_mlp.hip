@@ -1345,18 +1345,20 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
     const int n = j.n, k = j.k;
     const int KS = cdiv(k, KSTEP), NTp = cdiv(n, 16);
     const int NS = cdiv(n, KSTEP), KTp = rup(cdiv(k, 16), 8);
-    const int64_t tot = linear_pack_elems(n, k, dtype_id<T>());
+    // one Linear's pack is far below 2^31 elements: 32-bit index math (64-bit divisions by the
+    // runtime KS / NS cost tens of instructions each)
+    const int tot = (int)linear_pack_elems(n, k, dtype_id<T>());
     T* dst = reinterpret_cast<T*>(j.dst);
     T* dstT = reinterpret_cast<T*>(j.dstT);
-    for (int64_t e = (int64_t)blockIdx.x * MGN_THREADS + threadIdx.x; e < tot; e += (int64_t)gridDim.x * MGN_THREADS) {
-        const int v = (int)(e % VEC);
-        const int64_t fl = e / VEC;
-        const int lane = (int)(fl % 64);
-        const int64_t tile = fl / 64;
+    for (int e = blockIdx.x * MGN_THREADS + threadIdx.x; e < tot; e += gridDim.x * MGN_THREADS) {
+        const int v = e % VEC;
+        const int fl = e / VEC;
+        const int lane = fl % 64;
+        const int tile = fl / 64;
         {  // forward: tile = nt*KS + ks
             float w = 0.f;
-            if (tile < (int64_t)NTp * KS) {
-                const int nt = (int)(tile / KS), ks = (int)(tile % KS);
+            if (tile < NTp * KS) {
+                const int nt = tile / KS, ks = tile % KS;
                 const int nn = nt * 16 + (lane & 15), kk = ks * KSTEP + VEC * (lane >> 4) + v;
                 if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
             }
@@ -1364,8 +1366,8 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
         }
         {  // transposed: tile = kt*NS + ns
             float w = 0.f;
-            if (tile < (int64_t)KTp * NS) {
-                const int kt = (int)(tile / NS), ns = (int)(tile % NS);
+            if (tile < KTp * NS) {
+                const int kt = tile / NS, ns = tile % NS;
                 const int kk = kt * 16 + (lane & 15), nn = ns * KSTEP + VEC * (lane >> 4) + v;
                 if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
             }
