@@ -42,6 +42,13 @@ class TrainStep:
         if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
 
+    def _seed(self, loss):
+        """d loss / d loss = 1 from a resident tensor (autograd would launch a fill kernel per step)."""
+        one = getattr(self, "_one", None)
+        if one is None or one.device != loss.device or one.dtype != loss.dtype:
+            one = self._one = torch.ones_like(loss)
+        return one
+
     def _loss(self):
         net, tdn, _ = self.sim(self.batch)
         return masked_mse(tdn, net, self.node_type, self.masks, count=self._count)
@@ -56,7 +63,7 @@ class TrainStep:
         self.opt.zero_grad(set_to_none=True)
         self._prologue()
         loss = self._loss()
-        loss.backward()
+        loss.backward(self._seed(loss))
         if self.dp:
             allreduce_gradients(self.params, self.group)
         self.opt.step()
@@ -80,7 +87,7 @@ class TrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._loss()
-            loss.backward()
+            loss.backward(self._seed(loss))
             if not self.dp:
                 self.opt.launch()
         self.graph, self.static_loss = g, loss
