@@ -92,8 +92,9 @@ typedef struct mgn_mlp {
 /* Forward state kept for the backward. `act` holds the INPUT of every Linear (layer 0: the
  * MLP input — not for GraphNetBlock MLPs; layer l>0: the ReLU output of layer l-1) in the row-octet
  * layout (element (m,c) at ((m/8)*cols + c)*8 + m%8, rows padded to 64) that makes every weight-
- * gradient MFMA fragment one 16-byte load; `mask` holds the hidden layers' ReLU masks as 64-bit
- * wave-ballot words. Sizes: mgn_mlp_saved_elems(). */
+ * gradient MFMA fragment one 16-byte load; `mask` holds the hidden layers' ReLU masks (64-bit
+ * wave-ballot words, or the chained kernels' per-lane words — opaque to callers: only the backward of
+ * the same MLP reads it). Sizes: mgn_mlp_saved_elems(). */
 typedef struct mgn_mlp_saved {
     void* act;    /* act_elems elements of dtype                                             */
     void* mask;   /* mask_words x 8 bytes                                                    */
