@@ -639,6 +639,8 @@ def test_fused_simulator_preamble_bitwise(edge_norm):
     from graphphysics.utils import meshes
     from graphphysics.utils.data import Data
 
+    if os.environ.get("MGN_FUSED_PREAMBLE", "1") == "0":
+        pytest.skip("fused preamble disabled (MGN_FUSED_PREAMBLE=0)")
     b = meshes.cylinder_batch(3, jitter=0.01)
     data = Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})
     sims = []
