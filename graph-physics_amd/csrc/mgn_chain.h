@@ -1,4 +1,4 @@
-// Internal interface of the register-chained bf16 h=128 edge-MLP kernels (mgn_chain.hip).
+// Internal interface of the register-chained bf16 h=128 MLP kernels (mgn_chain16.hip).
 #pragma once
 #include "mgn_common.h"
 
@@ -19,10 +19,8 @@ struct ChainFwdArgs {
     float* rden_save;           // [M]
     __bf16* act8;               // R8 saved inputs of layers 1..3
     int64_t act_off[4];
-    unsigned long long* mask;   // [3][ntiles*64]: lane-owned ReLU bits
-    unsigned* mask32;           // 16-row variant: [3][ntiles16*64] 32-bit lane words
+    unsigned* mask32;           // [3][ntiles*64] 32-bit lane words (ReLU bits)
     int64_t mask_stride;        // 64-bit words per layer
-    int32_t ablate;             // diagnostics only (env MGN_ABLATE): 1 loads, 2 R8 saves, 4 MFMA, 8 row stores
 };
 
 struct ChainBwdArgs {
@@ -33,7 +31,6 @@ struct ChainBwdArgs {
     const float* rden_save;
     const float* scale;
     float dinv;
-    const unsigned long long* mask;
     const unsigned* mask32;
     int64_t mask_stride;
     const __bf16* wtpack;       // transposed 16x16x32 fragments of the 4 layers
@@ -45,7 +42,6 @@ struct ChainBwdArgs {
     float* dscale_part;         // [grid][128]
     __bf16* de;                 // [M][128] de_out + dZ0·W0a
     __bf16* dz0;                // [M][128] dZ0 row-major
-    int32_t ablate;             // as ChainFwdArgs
 };
 
 // Node MLP (16-row chained kernels): in = [x ‖ aggr], aggr[v] = Σ_{k: dst(k)=v} s_e ⊙ z_k / q_k
@@ -98,21 +94,13 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
                          hipStream_t st);
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
                           float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
-int chain_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
-                       int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
+// edge MLP forward / backward: 16x16x32 tiles, 12 waves per workgroup (three per SIMD);
 // nparts: number of dscale partial rows written (the reduction's row count)
-int chain_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
-                        const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                        hipStream_t st);
-size_t chain_lds_bytes();
-// 16-row variant (mgn_chain16.hip): same contracts, 16x16x32 tiles, two waves per SIMD
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
                          int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
                           hipStream_t st);
-// which chained variant block forward/backward use (read once; env MGN_CHAIN=32 or 16)
-int chain_variant();
 // dense MLP in_dim <= 32 -> 128 -> 128 -> 128 -> 128 + RMSNorm, bf16 (the encoders): 16-row chained
 // kernels with the generic DENSE save layout (ReLU masks: chained lane words)
 bool chain_dense_eligible(const mgn_mlp* m);

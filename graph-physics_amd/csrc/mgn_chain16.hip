@@ -327,22 +327,20 @@ int chain16_grid(int64_t ntiles, int nwk = NW) {
     return (int)(groups < cus ? groups : cus);
 }
 
-// waves per workgroup of the edge kernels, read once per process: 12 (three per SIMD) for both. Cfg B:
-// forward 40.9 vs 42.5 us at 8; backward 47.9 vs 50.6 us, with its d_aggr gather loaded by the tile
-// instead of prefetched (prefetched, the 168-VGPR cap spills 17 registers: 54.7 us).
-// env MGN_EDGE_WAVES / MGN_EDGE_BWD_WAVES = 8 or 12 override, for A/B
-static int waves_env(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e && (atoi(e) == 8 || atoi(e) == 12) ? atoi(e) : dflt;
-}
-int edge_waves() {
-    static const int v = waves_env("MGN_EDGE_WAVES", 12);
-    return v;
-}
-int edge_bwd_waves() {
-    static const int v = waves_env("MGN_EDGE_BWD_WAVES", 12);
-    return v;
-}
+// waves per workgroup of the edge kernels: 12 (three per SIMD) for both. Cfg B: forward 40.9 vs
+// 42.5 us at 8; backward 47.9 vs 50.6 us, with its d_aggr gather loaded by the tile instead of
+// prefetched (prefetched, the 168-VGPR cap spills 17 registers: 54.7 us). Compile-time (A/B builds:
+// -DMGN_EDGE_WAVES=8 / -DMGN_EDGE_BWD_WAVES=8); no runtime switch.
+#ifndef MGN_EDGE_WAVES
+#define MGN_EDGE_WAVES 12
+#endif
+#ifndef MGN_EDGE_BWD_WAVES
+#define MGN_EDGE_BWD_WAVES 12
+#endif
+static_assert((MGN_EDGE_WAVES == 8 || MGN_EDGE_WAVES == 12) && (MGN_EDGE_BWD_WAVES == 8 || MGN_EDGE_BWD_WAVES == 12),
+              "edge kernels run 8 or 12 waves per workgroup");
+constexpr int edge_waves() { return MGN_EDGE_WAVES; }
+constexpr int edge_bwd_waves() { return MGN_EDGE_BWD_WAVES; }
 
 void layer_offsets(const mgn_mlp* m, int64_t* woff, int* wks) {
     int64_t o = 0;
@@ -1446,15 +1444,20 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     return 0;
 }
 
-// the encoders' shape on the chained kernels (env MGN_CHAIN_DENSE=0: generic kernels, for A/B);
-// read once, like chain_variant(): forward and backward must agree on the ReLU-mask layout
+// the encoders' shape on the chained kernels (compile-time -DMGN_CHAIN_DENSE=0: generic kernels, for
+// A/B builds); forward and backward must agree on the ReLU-mask layout
+#ifndef MGN_CHAIN_DENSE
+#define MGN_CHAIN_DENSE 1
+#endif
 bool chain_dense_eligible(const mgn_mlp* m) {
-    static const bool on = [] {
-        const char* e = getenv("MGN_CHAIN_DENSE");
-        return !(e && atoi(e) == 0);
-    }();
-    return on && m->dtype == MGN_BF16 && m->hidden == H && m->out_dim == H && m->n_layers == 4 && m->has_norm &&
-           m->in_dim >= 1 && m->in_dim <= 32 && chain_variant() == 16;
+    return MGN_CHAIN_DENSE && m->dtype == MGN_BF16 && m->hidden == H && m->out_dim == H && m->n_layers == 4 &&
+           m->has_norm && m->in_dim >= 1 && m->in_dim <= 32;
+}
+
+// the GraphNetBlock edge MLP shape the chained edge kernels run: bf16, 3h -> h -> h -> h -> h + RMSNorm
+bool chain_eligible(const mgn_mlp* m) {
+    return m->dtype == MGN_BF16 && m->hidden == H && m->in_dim == 3 * H && m->out_dim == H && m->n_layers == 4 &&
+           m->has_norm;
 }
 
 int chain16_dense_forward(const mgn_mlp* m, const void* in, int in_dtype, int64_t in_ld, const int32_t* in_rows,

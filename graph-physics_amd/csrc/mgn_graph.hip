@@ -25,7 +25,7 @@ __global__ void split_edge_index(const int64_t* __restrict__ ei, int64_t E, int6
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= E) return;
     const int64_t r = ei[k], c = ei[E + k];
-    if (r < 0 || r >= N || c < 0 || c >= N) atomicOr(bad, 1u);
+    if (r < 0 || r >= N || c < 0 || c >= N) atomicOr(bad, MGN_ERR_EDGE_INDEX);
     src[k] = (int32_t)(r < 0 ? 0 : (r >= N ? N - 1 : r));
     dst[k] = (int32_t)(c < 0 ? 0 : (c >= N ? N - 1 : c));
     iota[k] = (int32_t)k;
@@ -288,6 +288,7 @@ struct PreSrc {
 };
 struct PreArgs {
     PreSrc s[3];
+    unsigned* err;  // device error word (MGN_ERR_TYPE_*), or NULL
     int32_t nsrc, accumulate;
     int64_t apply0[4];  // flat element offsets of the sources in the apply launch
 };
@@ -300,6 +301,16 @@ __device__ __forceinline__ float pre_value(const PreSrc& q, int which, int64_t r
         return t == (int64_t)(c - q.nf) ? 1.f : 0.f;
     }
     return q.a[r * q.lda + c];
+}
+
+// F.one_hot(node_type.long(), n_types) validation (reference simulator.py one-hot; ATen raises
+// "Class values must be non-negative." / "... smaller than num_classes."): flag the error word
+// instead of reading back to the host; the row's one-hot stays all-zero, so every access is in range.
+__device__ __forceinline__ void check_type(const PreSrc& q, int64_t r, unsigned* err) {
+    if (!err) return;
+    const float t = truncf(q.a[r * q.lda + q.nti]);
+    if (!(t >= 0.f)) atomicOr(err, MGN_ERR_TYPE_NEG);  // negative or NaN
+    else if (t >= (float)q.ntypes) atomicOr(err, MGN_ERR_TYPE_BIG);
 }
 
 __global__ __launch_bounds__(256) void preamble_stats(PreArgs a) {
@@ -320,6 +331,8 @@ __global__ __launch_bounds__(256) void preamble_stats(PreArgs a) {
             s += v;
             s2 = fmaf(v, v, s2);
         }
+        if (w == 1 && c == q.nf)
+            for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) check_type(q, r, a.err);
         red[c][threadIdx.x] = s;
         red[cols + c][threadIdx.x] = s2;
     }
@@ -362,6 +375,7 @@ __global__ __launch_bounds__(256) void preamble_apply(PreArgs a) {
     const int64_t i = k - a.apply0[w];
     const int64_t r = i / q.cols;
     const int c = (int)(i - r * q.cols);
+    if (w == 1 && c == q.nf) check_type(q, r, a.err);
     q.out[i] = (pre_value(q, w, r, c) - q.mstd[c]) / q.mstd[q.cols + c];
 }
 
@@ -476,14 +490,17 @@ size_t mgn_topology_workspace_bytes(int64_t E, int64_t N) {
     return al(sizeof(unsigned)) + 4 * al((size_t)E * 4) + al(radix_tmp_bytes(E));
 }
 
-int mgn_topology_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t* csc_src, int32_t* csc_dst,
-                       int32_t* csc_eid, int32_t* col_ptr, int32_t* row_ptr, int32_t* row_perm, void* ws,
-                       size_t ws_bytes, mgn_stream_t stream) {
+// edge_index validation flags MGN_ERR_EDGE_INDEX into the caller's device word (no host read-back);
+// out-of-range indices are clamped into [0, N) so every later kernel stays in bounds.
+int mgn_topology_build_async(const int64_t* edge_index, int64_t E, int64_t N, int32_t* csc_src, int32_t* csc_dst,
+                             int32_t* csc_eid, int32_t* col_ptr, int32_t* row_ptr, int32_t* row_perm, void* ws,
+                             size_t ws_bytes, uint32_t* err_word, mgn_stream_t stream) {
     MGN_REQUIRE(N >= 0 && E >= 0 && N < (1ll << 31) && E < (1ll << 31), "graph too large for int32 indices");
+    MGN_REQUIRE(N > 0 || E == 0, "edge_index out of range (edges on a graph without nodes)");
+    MGN_REQUIRE(err_word, "topology: NULL error word");
     MGN_REQUIRE(ws_bytes >= mgn_topology_workspace_bytes(E, N), "topology workspace too small");
     hipStream_t st = (hipStream_t)stream;
     char* w = reinterpret_cast<char*>(ws);
-    unsigned* bad = reinterpret_cast<unsigned*>(w);
     w += al(sizeof(unsigned));
     int32_t* src = reinterpret_cast<int32_t*>(w); w += al((size_t)E * 4);
     int32_t* dst = reinterpret_cast<int32_t*>(w); w += al((size_t)E * 4);
@@ -491,10 +508,10 @@ int mgn_topology_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t*
     int32_t* tmpk = reinterpret_cast<int32_t*>(w); w += al((size_t)E * 4);
     void* tmp = w;
     size_t tmp_bytes = radix_tmp_bytes(E);
-    MGN_TRY(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
     const unsigned eb = (unsigned)cdiv64(E, 256);
     if (E > 0) {
-        hipLaunchKernelGGL(split_edge_index, dim3(eb), dim3(256), 0, st, edge_index, E, N, src, dst, iota, bad);
+        hipLaunchKernelGGL(split_edge_index, dim3(eb), dim3(256), 0, st, edge_index, E, N, src, dst, iota,
+                           (unsigned*)err_word);
         MGN_LAUNCH_CHECK();
         // target-sorted order: stable sort of (col, eid)
         MGN_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, dst, csc_dst, iota, csc_eid, (int)E, 0, 32, st));
@@ -508,6 +525,19 @@ int mgn_topology_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t*
     MGN_LAUNCH_CHECK();
     hipLaunchKernelGGL(segment_ptr, dim3(nb), dim3(256), 0, st, tmpk, E, N, row_ptr);
     MGN_LAUNCH_CHECK();
+    return 0;
+}
+
+int mgn_topology_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t* csc_src, int32_t* csc_dst,
+                       int32_t* csc_eid, int32_t* col_ptr, int32_t* row_ptr, int32_t* row_perm, void* ws,
+                       size_t ws_bytes, mgn_stream_t stream) {
+    MGN_REQUIRE(ws_bytes >= mgn_topology_workspace_bytes(E, N), "topology workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    unsigned* bad = reinterpret_cast<unsigned*>(ws);  // the workspace's first word
+    MGN_TRY(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
+    const int rc = mgn_topology_build_async(edge_index, E, N, csc_src, csc_dst, csc_eid, col_ptr, row_ptr, row_perm,
+                                            ws, ws_bytes, bad, stream);
+    if (rc) return rc;
     unsigned hbad = 0;
     MGN_TRY(hipMemcpyAsync(&hbad, bad, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     MGN_TRY(hipStreamSynchronize(st));
@@ -629,7 +659,7 @@ size_t mgn_simulator_preamble_workspace_bytes(int64_t num_nodes, int64_t num_edg
 int mgn_simulator_statistics(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
                              int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end, const float* y,
                              int64_t ldy, const float* edge_attr, int64_t E, int32_t edge_cols, int64_t lde,
-                             float* packed, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+                             float* packed, uint32_t* err_word, void* ws, size_t ws_bytes, mgn_stream_t stream) {
     const int nf = feat_end - feat_start, no = out_end - out_start;
     MGN_REQUIRE(x && y && packed, "simulator statistics: NULL argument");
     MGN_REQUIRE(nf >= 0 && n_types >= 1 && nf + n_types <= STAT_MAXC && no >= 1 && no <= STAT_MAXC,
@@ -642,6 +672,7 @@ int mgn_simulator_statistics(const float* x, int64_t N, int64_t ldx, int32_t fea
     hipStream_t st = (hipStream_t)stream;
     PreArgs a;
     memset(&a, 0, sizeof(a));
+    a.err = err_word;
     a.nsrc = edge_attr ? 3 : 2;
     char* w = reinterpret_cast<char*>(ws);
     int blocks = 0;
@@ -678,8 +709,8 @@ int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_
                            int64_t ldy, const float* edge_attr, int64_t E, int32_t edge_cols, int64_t lde,
                            int32_t accumulate, const mgn_normalizer_state* out_norm,
                            const mgn_normalizer_state* node_norm, const mgn_normalizer_state* edge_norm,
-                           float* target_out, float* node_out, float* edge_out, void* ws, size_t ws_bytes,
-                           mgn_stream_t stream) {
+                           float* target_out, float* node_out, float* edge_out, uint32_t* err_word, void* ws,
+                           size_t ws_bytes, mgn_stream_t stream) {
     const int nf = feat_end - feat_start, no = out_end - out_start;
     MGN_REQUIRE(x && y && out_norm && node_norm && target_out && node_out, "simulator preamble: NULL argument");
     MGN_REQUIRE(nf >= 0 && n_types >= 1 && nf + n_types <= STAT_MAXC && no >= 1 && no <= STAT_MAXC,
@@ -692,6 +723,7 @@ int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_
     hipStream_t st = (hipStream_t)stream;
     PreArgs a;
     memset(&a, 0, sizeof(a));
+    a.err = err_word;
     a.accumulate = accumulate;
     const mgn_normalizer_state* ns[3] = {out_norm, node_norm, edge_norm};
     a.nsrc = edge_norm ? 3 : 2;

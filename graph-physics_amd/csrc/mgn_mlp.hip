@@ -240,15 +240,16 @@ struct FwdArgs {
     int64_t mask_stride;                 // words per hidden layer
     void* z_save;
     float* rden_save;
-    int32_t ablate;  // diagnostics only (env MGN_ABLATE): 1 gather, 2 R8 saves, 4 MFMA, 8 epilogue stores
+    int32_t ablate;  // diagnostics builds only (-DMGN_ABLATE=bits): 1 gather, 2 R8 saves, 4 MFMA, 8 epilogue stores
     int32_t r0_elems;  // LDS region 0 (layer-0 input / odd-layer activations / fp32 z staging), in T
 };
 
-// Diagnostic ablation mask for timing studies (results are wrong when nonzero).
-static int ablate_mask() {
-    const char* e = getenv("MGN_ABLATE");
-    return e ? atoi(e) : 0;
-}
+// Diagnostic ablation mask for timing studies (results are wrong when nonzero): a compile-time
+// define of diagnostics builds (MGN_ABLATE=bits python __graft_entry__.py), never a runtime switch.
+#ifndef MGN_ABLATE
+#define MGN_ABLATE 0
+#endif
+static int ablate_mask() { return MGN_ABLATE; }
 
 // Last layer: bias, RMSNorm, residual. z is staged (fp32) in LDS `zf` ([BM][H+4], aliases the
 // dead layer-0 input region), then one cooperative pass writes z, out = resid + scale*z/q and rden
@@ -2285,7 +2286,7 @@ static size_t block_fwd_ws(const mgn_topology* t, const mgn_mlp* edge) {
 }
 
 int mgn_block_forward_inference_supported(const mgn_mlp* edge, const mgn_mlp* node) {
-    return chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) ? 1 : 0;
+    return chain_eligible(edge) && chain_node_eligible(node) ? 1 : 0;
 }
 
 size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
@@ -2306,7 +2307,7 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     // inference (saved->edge.act == NULL): the chained bf16 h=128 kernels skip every backward save
     const bool infer = saved->edge.act == nullptr;
     MGN_REQUIRE(infer || saved->aggr, "block saved buffers missing");
-    MGN_REQUIRE(!infer || (chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) &&
+    MGN_REQUIRE(!infer || (chain_eligible(edge) && chain_node_eligible(node) &&
                            saved->node.act == nullptr),
                 "inference block forward (saved act = NULL) needs the chained bf16 h=128 path "
                 "(mgn_block_forward_inference_supported)");
@@ -2332,13 +2333,13 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     ein.proj_i = t->csc_dst;
     ein.proj_j = t->csc_src;
     if (chain) {
-        auto fwd = chain_variant() == 16 ? chain16_edge_forward : chain_edge_forward;
+        auto fwd = chain16_edge_forward;
         if (int r = fwd(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st)) return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
                                    nullptr, nullptr, st)) {
         return r;
     }
-    if (chain && chain_variant() == 16 && chain_node_eligible(node))
+    if (chain && chain_node_eligible(node))
         return chain16_node_forward(node, x, t, edge, &saved->edge, t->num_nodes, x_out, saved->aggr, &saved->node, st);
     MlpIn nin;
     memset(&nin, 0, sizeof(nin));
@@ -2391,7 +2392,7 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     if (int r = check_mlp(node)) return r;
     const BlockWs wl = block_ws_parts(t, edge, node);
     MGN_REQUIRE(ws_bytes >= wl.total, "block backward workspace too small");
-    MGN_REQUIRE(de_out || t->num_edges == 0 || (chain_eligible(edge) && chain_variant() == 16),
+    MGN_REQUIRE(de_out || t->num_edges == 0 || chain_eligible(edge),
                 "de_out = NULL (zero edge-output gradient) needs the chained bf16 h=128 edge MLP");
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
@@ -2413,7 +2414,7 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     on.mode = MODE_NODE;
     on.o1 = dx_part;
     on.o2 = d_aggr;
-    const bool chained = chain_eligible(edge) && chain_variant() == 16 && chain_node_eligible(node) &&
+    const bool chained = chain_eligible(edge) && chain_node_eligible(node) &&
                          t->num_nodes > 0 && t->num_edges > 0;
     void* ndz = nullptr;
     float* ndsp = nullptr;
@@ -2454,7 +2455,7 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
     oe.o1 = de;
     oe.o2 = dz0;
     if (chain_eligible(edge)) {
-        auto bwd = chain_variant() == 16 ? chain16_edge_backward : chain_edge_backward;
+        auto bwd = chain16_edge_backward;
         if (int r = bwd(edge, E, &saved->edge, de_out, d_aggr, t->csc_dst, dz8, dsp, &ntiles, de, dz0, st)) return r;
     } else if (E > 0) {
         if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, dz8, dsp, st)) return r;

@@ -58,6 +58,7 @@ EXPORTS = {
     "mgn_last_error": (ctypes.c_char_p, []),
     "mgn_topology_workspace_bytes": (_sz, [_i64, _i64]),
     "mgn_topology_build": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "mgn_topology_build_async": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     "mgn_linear_pack_elems": (_i64, [_i32, _i32, _i32]),
     "mgn_mlp_pack_elems": (_i64, [ctypes.POINTER(Mlp)]),
     "mgn_pack_weights": (_i32, [_vp, _i32, _i64, _vp]),
@@ -88,9 +89,9 @@ EXPORTS = {
     "mgn_simulator_preamble": (_i32, [_vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64,
                                       _i32, _i64, _i32, ctypes.POINTER(NormalizerState),
                                       ctypes.POINTER(NormalizerState), ctypes.POINTER(NormalizerState), _vp, _vp,
-                                      _vp, _vp, _sz, _vp]),
+                                      _vp, _vp, _vp, _sz, _vp]),
     "mgn_simulator_statistics": (_i32, [_vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64,
-                                        _i32, _i64, _vp, _vp, _sz, _vp]),
+                                        _i32, _i64, _vp, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_workspace_bytes": (_sz, [_i64]),
     "mgn_masked_mse": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
@@ -159,6 +160,99 @@ def check(rc):
         if "out of range" in msg:
             raise IndexError(msg)
         raise RuntimeError(f"libmgn error {rc}: {msg}")
+
+
+# ---------------------------------------------------------------- device error word (ABI v7)
+ERR_EDGE_INDEX, ERR_TYPE_NEG, ERR_TYPE_BIG = 1, 2, 4
+
+
+def _raise_for(bits):
+    """The exception the reference raises for the validation failure in `bits`."""
+    if bits & ERR_EDGE_INDEX:
+        raise IndexError("edge_index out of range: an index is outside [0, num_nodes) "
+                         "(libmgn device check; the reference's ATen gather raises IndexError)")
+    if bits & ERR_TYPE_NEG:
+        raise RuntimeError("Class values must be non-negative.")  # F.one_hot (reference simulator one-hot)
+    if bits & ERR_TYPE_BIG:
+        raise RuntimeError("Class values must be smaller than num_classes.")
+
+
+class ErrorWord:
+    """One uint32 device word per device that libmgn's validating kernels OR MGN_ERR_* bits into
+    (mgn_topology_build_async, mgn_simulator_preamble / _statistics), so a new batch never forces a
+    host read-back. arm() queues a non-blocking copy to pinned host memory behind the launches;
+    poll() raises (and clears the word) once a queued copy has landed with a bit set — at most one
+    call late, without synchronising; check() synchronises and raises now."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.event = None
+
+    def ptr(self):
+        return _vp(self.dev.data_ptr())
+
+    def arm(self):
+        """Queue the device word's copy-back (skipped while a hipGraph is being captured: a captured
+        step's owner arms after each replay)."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.host.copy_(self.dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.event = ev
+
+    def poll(self):
+        ev = self.event
+        if ev is None or not ev.query():
+            return
+        self.event = None
+        bits = int(self.host[0])
+        if bits:
+            self._clear()
+            _raise_for(bits)
+
+    def check(self):
+        if torch.cuda.is_current_stream_capturing():
+            return
+        torch.cuda.current_stream(self.device).synchronize()
+        bits = int(self.dev[0].item())
+        self.event = None
+        if bits:
+            self._clear()
+            _raise_for(bits)
+
+    def _clear(self):
+        self.dev.zero_()
+        self.host.zero_()
+
+
+_ERR_WORDS = {}
+
+
+def error_word(device):
+    d = torch.device(device)
+    if d.index is None:
+        d = torch.device(d.type, torch.cuda.current_device())
+    w = _ERR_WORDS.get(d)
+    if w is None:
+        w = _ERR_WORDS[d] = ErrorWord(d)
+    return w
+
+
+def poll_errors(device=None):
+    """Raise a validation error some earlier libmgn launch flagged, if its copy-back has landed."""
+    for d, w in list(_ERR_WORDS.items()):
+        if device is None or torch.device(device) == d or torch.device(device).index is None:
+            w.poll()
+
+
+def check_errors(device=None):
+    """Synchronise and raise any validation error libmgn flagged on the device word(s)."""
+    for d, w in list(_ERR_WORDS.items()):
+        if device is None or torch.device(device) == d or torch.device(device).index is None:
+            w.check()
 
 
 def require_device(t):
@@ -237,8 +331,9 @@ def simulator_preamble(x, y, edge_attr, feat, out, type_index, n_types, accumula
         ptr(x), N, x.stride(0), feat[0], feat[1], type_index, n_types, out[0], out[1], ptr(y), y.stride(0),
         ptr(edge_attr) if eo is not None else None, E, edge_attr.shape[1] if eo is not None else 0,
         edge_attr.stride(0) if eo is not None else 0, int(acc), ctypes.byref(st[0]), ctypes.byref(st[1]),
-        ctypes.byref(st[2]) if st[2] is not None else None, ptr(to), ptr(no), ptr(eo), ptr(ws), ws.numel(),
-        stream_ptr(dev)))
+        ctypes.byref(st[2]) if st[2] is not None else None, ptr(to), ptr(no), ptr(eo), error_word(dev).ptr(),
+        ptr(ws), ws.numel(), stream_ptr(dev)))
+    error_word(dev).arm()
     return to, no, eo
 
 
@@ -254,8 +349,9 @@ def simulator_statistics(x, y, edge_attr, feat, out, type_index, n_types, packed
     check(lib().mgn_simulator_statistics(
         ptr(x), N, x.stride(0), feat[0], feat[1], type_index, n_types, out[0], out[1], ptr(y), y.stride(0),
         ptr(edge_attr), E, edge_attr.shape[1] if edge_attr is not None else 0,
-        edge_attr.stride(0) if edge_attr is not None else 0, ptr(packed), ptr(ws), ws.numel(),
-        stream_ptr(x.device)))
+        edge_attr.stride(0) if edge_attr is not None else 0, ptr(packed), error_word(x.device).ptr(), ptr(ws),
+        ws.numel(), stream_ptr(x.device)))
+    error_word(x.device).arm()
     return packed
 
 

@@ -43,10 +43,17 @@ class GraphTopology:
         self.row_ptr = torch.empty(N + 1, **i32)
         wsb = L.mgn_topology_workspace_bytes(E, N)
         ws = torch.empty(max(int(wsb), 1), dtype=torch.uint8, device=dev)
-        nat.check(L.mgn_topology_build(
+        # no host read-back: an out-of-range index is flagged on the device error word (clamped in
+        # range meanwhile) and raised as IndexError by the next poll / check_errors()
+        ew = nat.error_word(dev)
+        ew.poll()
+        if E and N == 0:
+            raise IndexError("edge_index out of range: edges on a graph without nodes")
+        nat.check(L.mgn_topology_build_async(
             nat.ptr(ei), E, N, nat.ptr(self.csc_src), nat.ptr(self.csc_dst), nat.ptr(self.csc_eid),
-            nat.ptr(self.col_ptr), nat.ptr(self.row_ptr), nat.ptr(self.row_perm), nat.ptr(ws), wsb,
+            nat.ptr(self.col_ptr), nat.ptr(self.row_ptr), nat.ptr(self.row_perm), nat.ptr(ws), wsb, ew.ptr(),
             nat.stream_ptr(dev)))
+        ew.arm()
         self.struct = nat.Topology(N, E, self.csc_src.data_ptr(), self.csc_dst.data_ptr(),
                                    self.csc_eid.data_ptr(), self.col_ptr.data_ptr(),
                                    self.row_ptr.data_ptr(), self.row_perm.data_ptr())
@@ -434,9 +441,13 @@ class BlockFunction(torch.autograd.Function):
         H = espec.hidden
         N, E = topo.num_nodes, topo.num_edges
         x0 = x.detach().to(tdt).contiguous()
-        e0 = _permute(edge_attr.detach().contiguous(), topo.csc_eid, E, H,
-                      nat.mgn_dtype(edge_attr.dtype) if edge_attr.dtype in (torch.float32, torch.bfloat16)
-                      else nat.MGN_F32, tdt, False, st) if E else torch.empty((0, H), dtype=tdt, device=dev)
+        ea = edge_attr.detach()
+        if ea.dtype not in (torch.float32, torch.bfloat16):  # fp16 (autocast), fp64, ...: read as fp32
+            ea = ea.float()
+        if ea.dim() != 2 or ea.shape[0] != E or ea.shape[1] != H:
+            raise ValueError(f"edge_attr must have shape [{E}, {H}], got {list(ea.shape)}")
+        e0 = _permute(ea.contiguous(), topo.csc_eid, E, H, nat.mgn_dtype(ea.dtype), tdt, False, st) if E else \
+            torch.empty((0, H), dtype=tdt, device=dev)
         train = any(ctx.needs_input_grad)
         if not train and nat.lib().mgn_block_forward_inference_supported(ctypes.byref(pw.descs[0]),
                                                                          ctypes.byref(pw.descs[1])):

@@ -79,6 +79,7 @@ class Normalizer(nn.Module):
         self.process_group = None
         self._pending = None  # (sum, sum_sq, count) of the global batch, set by set_pending()
         self._pending_packed = None  # the same three as one [2*size + 1] tensor (views above)
+        self._pending_fresh = False  # refreshed for the next accumulating forward (one-shot)
         self._eps_cache = None
 
     def batch_statistics(self, d: torch.Tensor):
@@ -104,6 +105,7 @@ class Normalizer(nn.Module):
         self._pending[0].copy_(s)
         self._pending[1].copy_(s2)
         self._pending[2].copy_(cnt.reshape(()))
+        self._pending_fresh = True
 
     def bind_pending(self, packed_view: torch.Tensor):
         """Keep the pending statistics in `packed_view` (float32 [2*size + 1], e.g. a slice of one
@@ -113,9 +115,25 @@ class Normalizer(nn.Module):
         self._pending = (packed_view[:k].view_as(self._acc_sum), packed_view[k:2 * k].view_as(self._acc_sum_squared),
                          packed_view[2 * k])
 
+    def mark_pending_fresh(self):
+        """The bound pending buffer now holds this step's (exchanged) statistics."""
+        self._pending_fresh = True
+
     def clear_pending(self):
         self._pending = None
         self._pending_packed = None
+        self._pending_fresh = False
+
+    def _consume_pending(self):
+        """Pending statistics feed exactly ONE accumulating forward: a second forward without a new
+        exchange would re-add the previous batch's statistics (a hipGraph replay re-reads the bound
+        buffer, which its owner refreshes before every replay)."""
+        if self._pending is None or (self._pending[0].is_cuda and torch.cuda.is_current_stream_capturing()):
+            return
+        if not self._pending_fresh:
+            raise RuntimeError(f"{self.name}: pending batch statistics were already consumed; exchange "
+                               "them (Simulator.exchange_statistics) before every training forward")
+        self._pending_fresh = False
 
     def _eps(self) -> float:
         t = self._std_epsilon
@@ -132,6 +150,8 @@ class Normalizer(nn.Module):
         return all(b.dtype == torch.float32 and b.is_contiguous() and b.device == d.device for b in bufs)
 
     def forward(self, batched_data: torch.Tensor, accumulate: bool = True) -> torch.Tensor:
+        if accumulate:
+            self._consume_pending()
         if self._native_ok(batched_data, accumulate):
             from graphphysics import _native as nat  # one native pass: statistics, _accumulate, normalise
 

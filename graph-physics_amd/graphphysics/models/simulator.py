@@ -42,6 +42,8 @@ class Simulator(nn.Module):
         for n in (self._output_normalizer, self._node_normalizer, self._edge_normalizer):
             if n is not None:
                 n.process_group = group
+                if group is None:  # leaving data-parallel mode: no exchanged statistics linger
+                    n.clear_pending()
 
     def normalizers(self):
         return [n for n in (self._output_normalizer, self._node_normalizer, self._edge_normalizer)
@@ -78,6 +80,8 @@ class Simulator(nn.Module):
                                      NodeType.SIZE, buf)
             if dist.is_available() and dist.is_initialized():
                 dist.all_reduce(buf, group=group)
+            for n in norms:
+                n.mark_pending_fresh()
             return
         delta = inputs.y - self._get_pre_target(inputs)
         nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
@@ -128,6 +132,9 @@ class Simulator(nn.Module):
         if self._fused_preamble_ok(inputs, is_training):
             from graphphysics import _native as nat
 
+            if is_training:
+                for n in self.normalizers():
+                    n._consume_pending()
             tdn, nfn, ea = nat.simulator_preamble(
                 inputs.x, inputs.y, inputs.edge_attr, (self.feature_index_start, self.feature_index_end),
                 (self.output_index_start, self.output_index_end), self.node_type_index, NodeType.SIZE,
@@ -148,6 +155,10 @@ class Simulator(nn.Module):
         return self._get_pre_target(inputs) + self._output_normalizer.inverse(network_output)
 
     def forward(self, inputs) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+        if inputs.x.is_cuda:  # a validation error flagged by an earlier launch (no host sync)
+            from graphphysics import _native as nat
+
+            nat.poll_errors(inputs.x.device)
         graph, tdn = self._build_input_graph(inputs=inputs, is_training=self.training)
         net = self.model(graph)
         if self.training:
@@ -168,7 +179,13 @@ class Simulator(nn.Module):
             st, nrm = ck.get(key, {}), getattr(self, key, None)
             if nrm is not None and st:
                 for k, v in st.items():
-                    setattr(nrm, k, v)
+                    cur = getattr(nrm, k, None)
+                    if isinstance(cur, torch.Tensor) and isinstance(v, torch.Tensor) and cur.shape == v.shape:
+                        # in place: captured TrainStep / rollout graphs keep reading these buffers
+                        with torch.no_grad():
+                            cur.copy_(v.to(cur.device, cur.dtype))
+                    else:
+                        setattr(nrm, k, v)
 
     def save_checkpoint(self, savedir: Optional[str] = None) -> None:
         savedir = savedir or self.model_dir

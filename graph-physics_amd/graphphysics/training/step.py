@@ -15,11 +15,20 @@ only on the batch, so Simulator.exchange_statistics() sums them over ranks (one 
 before the replay; the global masked-node count is fixed per batch; the replay covers forward,
 loss and backward; then ONE all-reduce of the flat gradient buffer and the AdamW launch.
 `graph=False`: the same exchanges, fully eager.
+
+capture() warms the allocator and the library up with `warmup` eager steps and then RESTORES every
+piece of state they touched (parameters, optimizer moments and step count, scheduler, learning rate,
+normalizer buffers), so N calls are exactly N reference updates. The captured step owns one flat
+gradient buffer; the all-reduce and AdamW always read THAT buffer (re-pointing p.grad at it when
+eager() or zero_grad() moved it). Validation errors flagged on libmgn's device error word (node types
+outside the one-hot range) surface as the reference's RuntimeError at most one step late, without a
+host synchronisation per step.
 """
 import torch
 import torch.distributed as dist
 
-from graphphysics.training.distributed import allreduce_gradients, global_mask_count
+from graphphysics import _native as nat
+from graphphysics.training.distributed import allreduce_gradients, flat_grad_buffer, global_mask_count
 from graphphysics.utils.loss import masked_mse
 from graphphysics.utils.nodetype import NodeType
 
@@ -39,6 +48,8 @@ class TrainStep:
         self.graph = None
         self.static_loss = None
         self._count = None
+        self._graph_grads = None  # p.grad views of the captured step's flat gradient buffer
+        self._gflat = None
         if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
 
@@ -60,6 +71,7 @@ class TrainStep:
             self.sim.exchange_statistics(self.batch, self.group)
 
     def eager(self):
+        nat.poll_errors(self.batch.x.device)
         self.opt.zero_grad(set_to_none=True)
         self._prologue()
         loss = self._loss()
@@ -70,8 +82,41 @@ class TrainStep:
         self.sched.step()
         return loss
 
+    def _snapshot(self):
+        """Everything an eager step mutates: parameters + buffers (normalizer accumulators), the
+        optimizer's moments / step counts / learning rates, the scheduler."""
+        tensors = [t for t in list(self.sim.parameters()) + list(self.sim.buffers())]
+        groups = []
+        for g in self.opt.param_groups:
+            fs = g.get("flat_state")
+            groups.append((g.get("step_count"), g["lr"], fs, tuple(t.clone() for t in fs) if fs else None))
+        return ([t.detach().clone() for t in tensors], tensors, groups, self.sched.state_dict())
+
+    @torch.no_grad()
+    def _restore(self, snap):
+        vals, tensors, groups, sched = snap
+        for t, v in zip(tensors, vals):
+            t.copy_(v)
+        for g, (cnt, lr, fs, fsv) in zip(self.opt.param_groups, groups):
+            if cnt is None:
+                g.pop("step_count", None)
+            else:
+                g["step_count"] = cnt
+            g["lr"] = lr
+            cur = g.get("flat_state")
+            if cur is not None:
+                for t, v in zip(cur, fsv if fsv is not None else (None, None)):
+                    t.copy_(v) if v is not None else t.zero_()
+            for p in g["params"]:
+                st = self.opt.state.get(p)
+                if st is not None and "step" in st:
+                    st["step"] = torch.tensor(float(cnt or 0))
+        self.sched.load_state_dict(sched)
+
     def capture(self, warmup=2, on_record=None):
-        """Run `warmup` eager steps on a side stream (allocator + library state), then record."""
+        """Run `warmup` eager steps on a side stream (allocator + library state), restore the state
+        they changed (so they are not extra updates), then record one step."""
+        snap = self._snapshot()
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
@@ -80,6 +125,7 @@ class TrainStep:
                 self.eager()
         cur.wait_stream(side)
         torch.cuda.synchronize()
+        self._restore(snap)
         self.opt.zero_grad(set_to_none=True)
         if on_record is not None:
             on_record()
@@ -91,20 +137,36 @@ class TrainStep:
             if not self.dp:
                 self.opt.launch()
         self.graph, self.static_loss = g, loss
+        self._graph_grads = [p.grad for p in self.params]
+        self._gflat = flat_grad_buffer(self.params)
         return self
+
+    def _bind_graph_grads(self):
+        """p.grad -> the captured step's gradient buffer (eager() / zero_grad() may have moved it)."""
+        gg = self._graph_grads
+        if self.params[0].grad is not gg[0] or self.params[-1].grad is not gg[-1]:
+            for p, g in zip(self.params, gg):
+                p.grad = g
 
     def __call__(self):
         if not self.use_graph:
             return self.eager()
+        dev = self.batch.x.device
+        nat.poll_errors(dev)
         if self.graph is None:
             self.capture()
+        self._bind_graph_grads()
         self.opt.stage()
         if self.dp:
             self._prologue()
             self.graph.replay()
-            allreduce_gradients(self.params, self.group)
+            if self._gflat is not None and dist.is_available() and dist.is_initialized():
+                dist.all_reduce(self._gflat, group=self.group)
+            else:
+                allreduce_gradients(self.params, self.group)
             self.opt.launch()
         else:
             self.graph.replay()
+        nat.error_word(dev).arm()
         self.sched.step()
         return self.static_loss

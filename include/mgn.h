@@ -25,7 +25,12 @@
  *  - All device memory is owned by the caller (PyTorch caching allocator); raw pointers + sizes.
  *    The library holds no device allocations and no global mutable state besides the
  *    thread-local error string. Every call is asynchronous on the given stream except
- *    mgn_topology_build (which reads back one validation word).
+ *    mgn_topology_build (which reads back one validation word; mgn_topology_build_async does not).
+ *  - Input validation that needs the data (edge_index range, node-type range) never reads back to
+ *    the host on the asynchronous entry points: kernels OR an MGN_ERR_* bit into a caller-owned
+ *    device word (uint32, zeroed by the caller), keep every access in bounds (clamped index /
+ *    all-zero one-hot row), and the caller checks the word lazily and raises the reference's
+ *    exception (IndexError / RuntimeError).
  *  - Return value: 0 on success, otherwise a nonzero status; mgn_last_error() describes it.
  *  - Edge order inside the library is target-sorted ("CSC" order: stable sort of the caller's
  *    edges by edge_index[1]); csc_eid maps it back to the caller's order.
@@ -46,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 6
+#define MGN_ABI_VERSION 7
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -54,6 +59,11 @@ typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 /* ---------------------------------------------------------------- status */
 int mgn_abi_version(void);
 const char* mgn_last_error(void);
+
+/* bits of the device error word */
+#define MGN_ERR_EDGE_INDEX 1u /* edge_index outside [0, N): reference IndexError (ATen index)         */
+#define MGN_ERR_TYPE_NEG 2u   /* node type < 0 or NaN: F.one_hot "Class values must be non-negative." */
+#define MGN_ERR_TYPE_BIG 4u   /* node type >= n_types: "Class values must be smaller than num_classes." */
 
 /* ---------------------------------------------------------------- topology */
 typedef struct mgn_topology {
@@ -74,6 +84,13 @@ int mgn_topology_build(const int64_t* edge_index, int64_t num_edges, int64_t num
                        int32_t* csc_src, int32_t* csc_dst, int32_t* csc_eid, int32_t* col_ptr,
                        int32_t* row_ptr, int32_t* row_perm, void* ws, size_t ws_bytes,
                        mgn_stream_t stream);
+/* The same without any host read-back (a new batch's topology never synchronises): an index
+ * outside [0, N) sets MGN_ERR_EDGE_INDEX in *err_word and is clamped into range. Host-side
+ * failures (sizes, N = 0 with E > 0) still return a nonzero status. */
+int mgn_topology_build_async(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                             int32_t* csc_src, int32_t* csc_dst, int32_t* csc_eid, int32_t* col_ptr,
+                             int32_t* row_ptr, int32_t* row_perm, void* ws, size_t ws_bytes,
+                             uint32_t* err_word, mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- MLP (build_mlp) */
 typedef struct mgn_mlp {
@@ -204,7 +221,8 @@ int mgn_normalizer_forward(const float* x, int64_t rows, int32_t cols, int64_t l
  * read straight from x [N, ldx], y [N, ldy] and edge_attr (no intermediate tensors), in 3 launches.
  * Statistics, buffers and outputs are bit-identical to the torch expressions + three
  * mgn_normalizer_forward calls (same partition and order). A node type outside [0, n_types) gives an
- * all-zero one-hot row (the reference's F.one_hot raises). Output columns <= 32 per normalizer. */
+ * all-zero one-hot row and sets MGN_ERR_TYPE_NEG / MGN_ERR_TYPE_BIG in *err_word (if non-NULL); the
+ * caller raises F.one_hot's RuntimeError from it. Output columns <= 32 per normalizer. */
 typedef struct mgn_normalizer_state {
     float* acc_sum;      /* [cols] */
     float* acc_sum_sq;   /* [cols] */
@@ -220,18 +238,20 @@ int mgn_simulator_preamble(const float* x, int64_t N, int64_t ldx, int32_t feat_
                            int32_t edge_cols, int64_t lde, int32_t accumulate,
                            const mgn_normalizer_state* out_norm, const mgn_normalizer_state* node_norm,
                            const mgn_normalizer_state* edge_norm, float* target_out, float* node_out,
-                           float* edge_out, void* ws, size_t ws_bytes, mgn_stream_t stream);
+                           float* edge_out, uint32_t* err_word, void* ws, size_t ws_bytes,
+                           mgn_stream_t stream);
 
 /* The batch statistics of the same three normalizers without updating them (the data-parallel
  * prologue: summed over ranks, then handed to mgn_simulator_preamble as `pending`): packed =
  * [Σ target delta, Σ target delta², N, Σ node features, Σ node features², N, (Σ edge_attr,
  * Σ edge_attr², E if edge_attr != NULL)] — each block the float[2*cols + 1] layout of `pending`, with
- * the same sums as mgn_column_stats. Workspace: mgn_simulator_preamble_workspace_bytes. */
+ * the same sums as mgn_column_stats. Workspace: mgn_simulator_preamble_workspace_bytes. Node types
+ * are validated as in mgn_simulator_preamble (err_word may be NULL). */
 int mgn_simulator_statistics(const float* x, int64_t N, int64_t ldx, int32_t feat_start, int32_t feat_end,
                              int32_t type_index, int32_t n_types, int32_t out_start, int32_t out_end,
                              const float* y, int64_t ldy, const float* edge_attr, int64_t E,
-                             int32_t edge_cols, int64_t lde, float* packed, void* ws, size_t ws_bytes,
-                             mgn_stream_t stream);
+                             int32_t edge_cols, int64_t lde, float* packed, uint32_t* err_word, void* ws,
+                             size_t ws_bytes, mgn_stream_t stream);
 
 /* Masked L2 loss (reference utils/loss.py:10-65): *loss = Σ_r m_r Σ_c (pred - target)² / (count ·
  * cols) over row-major fp32 [rows, cols] pred/target, m_r = 1 when node_type[r·nt_ld] (a float

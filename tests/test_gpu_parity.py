@@ -94,10 +94,25 @@ def test_topology_matches_stable_sort():
 
 
 def test_topology_rejects_out_of_range():
+    """mgn_topology_build_async never reads back: the range check lands on the device error word
+    (indices clamped meanwhile, so nothing downstream reads out of bounds) and raises IndexError like
+    the reference's ATen gather at the next check — synchronous check_errors() or a later poll."""
+    from graphphysics import _native as nat
     from graphphysics.models import _engine
 
+    t = _engine.GraphTopology(torch.tensor([[0, 1], [1, 5]], device=DEV), 4)
+    assert int(t.csc_dst.max()) <= 3  # clamped into range
     with pytest.raises(IndexError):
-        _engine.GraphTopology(torch.tensor([[0, 1], [1, 5]], device=DEV), 4)
+        nat.check_errors(DEV)
+    nat.check_errors(DEV)  # the word was cleared by the raise
+    # lazily: the next libmgn call that polls raises, without any synchronisation in between
+    _engine.GraphTopology(torch.tensor([[0, 1], [7, 0]], device=DEV), 4)
+    torch.cuda.synchronize()
+    with pytest.raises(IndexError):
+        _engine.GraphTopology(torch.tensor([[0, 1], [1, 0]], device=DEV), 4)
+    nat.check_errors(DEV)
+    with pytest.raises(IndexError):  # edges on a graph without nodes: host-side, immediate
+        _engine.GraphTopology(torch.tensor([[0], [0]], device=DEV), 0)
 
 
 # ----------------------------------------------------------------------------- block
@@ -379,13 +394,100 @@ def test_captured_step_equals_eager_step():
     for graph in (False, True):
         sim, opt, sch, data = _cyl_train_setup(torch.float32)
         st = TrainStep(sim, opt, sch, data, graph=graph)
-        # captured: capture() runs 2 eager warm-up steps (real steps), then replays
-        losses = [float(st().item()) for _ in range(5 if graph else 7)]
+        # capture()'s eager warm-up steps are undone: 5 calls = 5 reference updates either way
+        losses = [float(st().item()) for _ in range(5)]
         torch.cuda.synchronize()
-        res.append((losses[-5:], [p.detach().clone() for p in sim.parameters()]))
+        res.append((losses, [p.detach().clone() for p in sim.parameters()],
+                    [b.detach().clone() for b in sim.buffers()], opt.param_groups[0]["step_count"],
+                    sch.last_epoch, opt.param_groups[0]["lr"]))
     np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6)
     for a, b in zip(res[0][1], res[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+    for a, b in zip(res[0][2], res[1][2]):  # normalizer accumulators: 5 accumulations each
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
+    assert res[0][3:] == res[1][3:] and res[1][3] == 5
+
+
+def test_block_edge_attr_fp16_and_fp64_inputs():
+    """GraphNetBlock reads fp16 / fp64 edge_attr as fp32 (no reinterpretation of the
+    buffer), giving exactly the fp32-input result; a wrongly shaped edge_attr is rejected."""
+    from graphphysics.models.layers import GraphNetBlock
+
+    torch.manual_seed(0)
+    blk = GraphNetBlock(16).to(DEV)
+    n, e = 40, 150
+    x = torch.randn(n, 16, device=DEV)
+    ei = torch.randint(0, n, (2, e), device=DEV)
+    ea = torch.randn(e, 16, device=DEV).half()
+    with torch.no_grad():
+        x32, e32 = blk(x, ei, ea.float())
+        for t in (ea, ea.double()):
+            x1, e1 = blk(x, ei, t)
+            assert torch.equal(x1, x32) and torch.equal(e1.float(), e32)
+        with pytest.raises(ValueError):
+            blk(x, ei, ea[:, :8].float())
+
+
+def test_eager_between_replays_keeps_graph_gradients():
+    """eager() or zero_grad(set_to_none) between replays must not leave the captured
+    step's all-reduce + AdamW reading stale or missing gradients (1-rank data-parallel step)."""
+    import torch.distributed as dist
+
+    from graphphysics.training.step import TrainStep
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 200))
+    res = []
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        for mix in (False, True):
+            sim, opt, sch, data = _cyl_train_setup(torch.float32)
+            st = TrainStep(sim, opt, sch, data, graph=True, data_parallel=True)
+            ref = TrainStep(sim, opt, sch, data, graph=False, data_parallel=True)
+            losses = []
+            for i in range(6):
+                if mix and i in (2, 4):
+                    losses.append(float(ref().item()))  # an eager step between replays
+                    opt.zero_grad(set_to_none=True)
+                else:
+                    losses.append(float(st().item()))
+            torch.cuda.synchronize()
+            res.append((losses, [p.detach().clone() for p in sim.parameters()]))
+    finally:
+        dist.destroy_process_group()
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-5)
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("bad,msg", [(9.0, "smaller than num_classes"), (-1.0, "non-negative"),
+                                     (float("nan"), "non-negative")])
+def test_invalid_node_type_raises_like_one_hot(bad, msg):
+    """The fused preamble validates node types the way F.one_hot(x[:, 2].long(), 9) does in the
+    reference Simulator, on the device error word (no per-step host read-back): eager forward ->
+    RuntimeError at check_errors(); captured TrainStep -> RuntimeError within one step."""
+    from graphphysics import _native as nat
+    from graphphysics.training.step import TrainStep
+
+    if os.environ.get("MGN_FUSED_PREAMBLE", "1") == "0":
+        pytest.skip("fused preamble disabled (MGN_FUSED_PREAMBLE=0)")
+    with pytest.raises(RuntimeError, match=msg):  # what the reference raises on the same value
+        torch.nn.functional.one_hot(torch.tensor([0.0, bad]).long(), 9)
+    sim, opt, sch, data = _cyl_train_setup(torch.float32)
+    x = data.x.clone()
+    x[7, 2] = bad
+    data.x = x
+    with torch.no_grad():
+        sim(data)
+    with pytest.raises(RuntimeError, match=msg):
+        nat.check_errors(DEV)
+    nat.check_errors(DEV)  # cleared
+    st = TrainStep(sim, opt, sch, data, graph=True)
+    with pytest.raises(RuntimeError, match=msg):
+        for _ in range(3):
+            st()
+            torch.cuda.synchronize()
+    nat.check_errors(DEV)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

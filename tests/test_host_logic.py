@@ -177,3 +177,47 @@ def test_product_path_refuses_cpu_tensors():
     with pytest.raises(RuntimeError, match="HIP device"):
         m(Data(x=torch.zeros(4, 5), edge_index=torch.zeros((2, 1), dtype=torch.long),
                edge_attr=torch.zeros(1, 3)))
+
+
+def test_pending_statistics_feed_one_forward_only():
+    """ADVICE r01: exchanged (pending) statistics are consumed by exactly one accumulating forward;
+    a second forward without a new exchange raises instead of silently re-adding them, and leaving
+    data-parallel mode clears them."""
+    from graphphysics.models.layers import Normalizer
+
+    n = Normalizer(3, device="cpu")
+    d = torch.randn(5, 3)
+    n.set_pending(d.sum(0, keepdim=True), (d ** 2).sum(0, keepdim=True), torch.tensor(5.0))
+    n(d)
+    with pytest.raises(RuntimeError, match="already consumed"):
+        n(d)
+    n(d, accumulate=False)  # evaluation never consumes
+    n.set_pending(d.sum(0, keepdim=True), (d ** 2).sum(0, keepdim=True), torch.tensor(5.0))
+    n(d)
+    n.clear_pending()
+    n(d)  # local statistics again
+    assert float(n._acc_count) == 15.0
+
+
+def test_load_checkpoint_updates_normalizer_buffers_in_place(tmp_path):
+    """load_checkpoint copies the normalizer statistics into the existing buffers, so a
+    captured step / rollout graph recorded before the load reads the loaded values."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+
+    def make():
+        torch.manual_seed(0)
+        return Simulator(11, 3, 2, 0, 2, 0, 2, 2, EncodeProcessDecode(2, 11, 3, 2, 8), torch.device("cpu"),
+                         model_dir=str(tmp_path / "sim.pth"))
+
+    a = make()
+    for nrm in a.normalizers():
+        nrm._acc_sum.uniform_()
+        nrm._acc_count.fill_(7.0)
+    a.save_checkpoint()
+    b = make()
+    before = [(nrm._acc_sum, nrm._acc_count) for nrm in b.normalizers()]
+    b.load_checkpoint()
+    for (s0, c0), na, nb in zip(before, a.normalizers(), b.normalizers()):
+        assert nb._acc_sum is s0 and nb._acc_count is c0
+        assert torch.equal(nb._acc_sum, na._acc_sum) and float(nb._acc_count) == 7.0
