@@ -44,15 +44,24 @@ def parse():
     ap.add_argument("--mp", type=int, default=15)
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU baseline steps (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=10,
+                    help="timed CPU baseline steps after 3 warm-up steps (SURVEY §8d; 0: skip)")
     ap.add_argument("--no-mse", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel step (exchanges + split graph) even on one rank")
-    ap.add_argument("--workload", default="cylinder", choices=["cylinder", "aneurysm"],
-                    help="cylinder: Cfg B (headline); aneurysm: Cfg E (1 k-hop-2 aneurysm graph per GPU)")
+    ap.add_argument("--workload", default="cylinder", choices=["cylinder", "aneurysm", "plate"],
+                    help="cylinder: Cfg B (headline); aneurysm: Cfg E (1 k-hop-2 aneurysm graph per GPU); "
+                         "plate: Cfg C (DeformingPlate-shaped tet mesh + world edges)")
+    ap.add_argument("--print-workload", action="store_true",
+                    help="print the workload key the PMC files are stamped with, and exit")
     return ap.parse_args()
+
+
+def workload_key(a):
+    """Stamp of the measured configuration (PMC files only apply to the same one)."""
+    return "%s:b%d:mp%d:h%d:%s" % (a.workload, a.batch if a.workload == "cylinder" else 1, a.mp, a.hidden, a.dtype)
 
 
 def make_workload(a, dev, rank, mesh):
@@ -73,6 +82,13 @@ def make_workload(a, dev, rank, mesh):
         return b, data, dict(node_in=11, edge_in=3, out=2, fs=(0, 2), os=(0, 2), nti=2), \
             "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, a.hidden, a.batch), \
             "%d jittered copies of the reference in-tree CylinderFlow mesh per GPU" % a.batch
+    if a.workload == "plate":
+        g, lay = meshes.plate_graph(dev, seed=rank)
+        b = {"x": g.x.cpu().numpy(), "y": g.y.cpu().numpy(), "edge_index": g.edge_index.cpu().numpy(),
+             "edge_attr": g.edge_attr.cpu().numpy()}
+        data = Data(x=g.x, y=g.y, edge_index=g.edge_index, edge_attr=g.edge_attr, pos=g.pos)
+        return b, data, lay, "DeformingPlate MGN %dMP h=%d, 1 graph per GPU, world edges (Cfg C)" % (a.mp, a.hidden), \
+            "DeformingPlate-shaped tet plate + obstacle (meshes.plate_sample), reference preprocessing on device"
     from graphphysics.utils import graph_build as G
 
     z = np.load(os.path.join(ROOT, "tests", "golden", "aneurysm_mesh.npz"))
@@ -93,30 +109,37 @@ def make_workload(a, dev, rank, mesh):
         "reference aneurysm mock mesh (k-hop 2 built on device), synthetic node features"
 
 
-def flops_per_block(n, e, h):
-    # MFMA FLOPs per launch (2·Σ in·out per row). The edge MLP's layer 0 runs on the e block only
-    # (the x blocks are applied per node: node_proj / node_grad kernels), so 4 128x128 Linears.
-    return 8 * h * h * e, 10 * h * h * n  # edge MLP, node MLP
+def class_work(n, e, h, mp, lay, nparams, nweights, es):
+    """Algorithmic work per STEP of every kernel class (SURVEY.md §8(a,d) per-unit figures x the units
+    the class processes; the reference algorithm's FLOPs, so the split-layer-0 reformulation is not
+    credited with work it skips): ("mfma", FLOPs) or ("hbm", bytes).
+      edge MLP 12h²/edge fwd (a2): fwd_edge does the e block of layer 0 + the 3 hidden Linears (8h²),
+      proj the x_i / x_j blocks of layer 0 (4h²/edge, applied per node); backward data the same split
+      (bwd_edge 8h², combine 4h²); weight gradients 12h²/edge + 10h²/node in one ring launch; node MLP
+      10h²/node (a3); encoders/decoder 2(in·h + 3h²) per row and 2(3h² + h·out) (a7).
+      AdamW: p, g, m, v read + p, m, v written (28 B/param); pack: fp32 weights in, 2 bf16 copies out."""
+    enc = 2 * (lay["edge_in"] * h + 3 * h * h) * e + 2 * (lay["node_in"] * h + 3 * h * h) * n
+    dec = 2 * (3 * h * h + h * lay["out"]) * n
+    return {
+        "fwd_edge": ("mfma", mp * 8 * h * h * e), "proj": ("mfma", mp * 4 * h * h * e),
+        "fwd_node": ("mfma", mp * 10 * h * h * n), "bwd_edge": ("mfma", mp * 8 * h * h * e),
+        "combine": ("mfma", mp * 4 * h * h * e), "bwd_node": ("mfma", mp * 10 * h * h * n),
+        "wgrad": ("mfma", mp * (12 * h * h * e + 10 * h * h * n)),
+        "fwd_dense": ("mfma", enc + dec), "bwd_dense": ("mfma", enc + dec), "wgrad_dense": ("mfma", enc + dec),
+        "adamw": ("hbm", 28 * nparams), "pack": ("hbm", 8 * nweights),
+    }
 
 
-def bytes_per_block(n, e, h, es):
-    """Compulsory HBM bytes per launch of the block kernels (SURVEY §8d unit = one edge / node):
-    every input read once, every output written once, gathered rows counted once per use at their
-    stored size; es = activation element size (2 bf16, 4 fp32)."""
-    mask = 3 * h // 8  # ReLU bits of the 3 hidden layers
-    edge_fwd = e * (es * h + es * h * 2 + 3 * es * h + mask + 4 + 2 * 4 * h)
-    # e in | out, z | R8 inputs of layers 1..3 | masks | rden | fp32 node projections P_i, P_j gathered
-    edge_bwd = e * (3 * es * h + 4 + mask + 3 * es * h + 2 * es * h)
-    # de_out, d_aggr[dst], z in | rden | masks | dZ of layers 1..3 (R8) | de, dZ0 row-major out
-    node_fwd = e * (es * h + 4) + n * (es * h + 3 * es * h + 4 + mask + 3 * es * h)
-    # edge z + rden (segment sum) | x in; x_out, aggr, z out; rden; masks; R8 inputs of layers 1..3
-    node_bwd = n * (es * h + es * h + 4 + mask + 4 * es * h + 2 * es * h)
-    # dx_out, z in | rden | masks | dZ of 4 layers (R8) | dx_part, d_aggr out
-    return {"fwd_edge": edge_fwd, "bwd_edge": edge_bwd, "fwd_node": node_fwd, "bwd_node": node_bwd}
+def scatter_bytes(n, e, h, es):
+    """SURVEY §8(a5,d): segmented-sum bytes per block forward, E·h·s + N·h·s + 4E + 4(N+1)."""
+    return e * h * es + n * h * es + 4 * e + 4 * (n + 1)
 
 
 def main():
     a = parse()
+    if a.print_workload:
+        print(workload_key(a))
+        return
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -207,31 +230,59 @@ def main():
         return
 
     h = a.hidden
-    fe, fn = flops_per_block(N, E, h)
-    alg_bytes = bytes_per_block(N, E, h, 2 if a.dtype == "bf16" else 4)
+    es = 2 if a.dtype == "bf16" else 4
+    nparams = sum(p.numel() for p in sim.parameters())
+    nweights = sum(m.weight.numel() for m in sim.model.modules() if isinstance(m, torch.nn.Linear))
+    work = class_work(N, E, h, a.mp, lay, nparams, nweights, es)
     kinds = {}
     for k, (ms, cnt) in prof.items():
         if cnt:
-            kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2)}
-    # algorithmic work per launch of each kernel class: MFMA FLOPs
-    alg_flops = {"fwd_edge": fe, "fwd_node": fn, "bwd_edge": fe, "bwd_node": fn}
+            kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2),
+                        "ms_per_step": round(ms / a.steps, 4)}
+            if k in work:
+                bound, amount = work[k]
+                per_s = amount * a.steps / (ms / 1000)
+                if bound == "mfma":
+                    kinds[k].update(bound="mfma", tflops=round(per_s / 1e12, 2),
+                                    frac=round(per_s / 1e12 / PEAK[a.dtype], 4))
+                else:
+                    kinds[k].update(bound="hbm", gbs=round(per_s / 1e9, 1), frac=round(per_s / 1e9 / HBM_PEAK, 4))
     roof = None
+    wl = workload_key(a)
+    step_flops = 3 * (a.mp * (12 * h * h * E + 10 * h * h * N) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
+                      + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
+    step_tf = step_flops * a.steps / dt / 1e12
     if kinds:
-        dom = max((k for k in kinds if k in alg_flops), key=lambda k: kinds[k]["total_ms"])
-        avg_s = kinds[dom]["total_ms"] / 1000 / kinds[dom]["launches"]
-        tf = alg_flops[dom] / avg_s / 1e12
-        gbs = alg_bytes[dom] / avg_s / 1e9
-        mfma = {"achieved": round(tf, 2), "peak": PEAK[a.dtype], "unit": "TFLOP/s", "frac": round(tf / PEAK[a.dtype], 4)}
-        hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbs / HBM_PEAK, 4)}
-        bound = "hbm" if hbm["frac"] >= mfma["frac"] else "mfma"
-        roof = {"kernel": dom, "bound": bound, **(hbm if bound == "hbm" else mfma), "traffic": None,
-                "bytes_per_launch": alg_bytes[dom], "flops_per_launch": alg_flops[dom],
-                "avg_launch_us": round(avg_s * 1e6, 2), "hbm": hbm, "mfma": mfma}
-        step_flops = 3 * (a.mp * (fe + fn) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
-                          + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
-        roof["step_tflops_per_s"] = round(step_flops * a.steps / dt / 1e12, 2)
-    if roof is not None:
-        roof["traffic"], roof["traffic_note"] = pmc_traffic(roof["kernel"])
+        # dominant kernel class = largest total time over ALL classes (rocprofv3 agrees: profiles/)
+        dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
+        kd = kinds[dom]
+        bound, amount = work.get(dom, ("mfma", 0))
+        per_launch = amount * a.steps / kd["launches"]
+        avg_s = kd["total_ms"] / 1000 / kd["launches"]
+        ach = per_launch / avg_s / (1e12 if bound == "mfma" else 1e9)
+        peak = PEAK[a.dtype] if bound == "mfma" else HBM_PEAK
+        pmc = pmc_lookup(dom, wl)
+        roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak,
+                "unit": "TFLOP/s" if bound == "mfma" else "GB/s", "frac": round(ach / peak, 4),
+                "traffic": pmc.get("hbm_bytes"), "traffic_source": pmc.get("source"),
+                "mfma_util_measured": pmc.get("mfma_util"),
+                ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per_launch,
+                "avg_launch_us": round(avg_s * 1e6, 2), "launches_per_step": kd["launches"] / a.steps,
+                "peak_source": "MI355X_MICROARCH.md: dense bf16 MFMA 2.5 PFLOP/s (fp32 MFMA 157.3), HBM3E 8 TB/s",
+                "step": {"tflops_per_s": round(step_tf, 2), "frac": round(step_tf / PEAK[a.dtype], 4),
+                         "flops_per_step": step_flops, "note": "3 x F_fwd (SURVEY §8d) / measured ms_per_step"}}
+        if "fwd_node" in kinds:  # the segmented sum is fused into the node-MLP forward (CSC segments)
+            sb = scatter_bytes(N, E, h, es)
+            t = kinds["fwd_node"]["total_ms"] / 1000 / kinds["fwd_node"]["launches"]
+            roof["scatter"] = {"kernel": "fwd_node (segment sum fused into the node-MLP forward)",
+                               "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
+                               "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
+        if "combine" in kinds:
+            sb = 2 * scatter_bytes(N, E, h, es)
+            t = kinds["combine"]["total_ms"] / 1000 / kinds["combine"]["launches"]
+            roof["gather_bwd"] = {"kernel": "combine (dP_i / dP_j segment sums over both index directions)",
+                                  "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
+                                  "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
     value = world * a.steps / dt
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
@@ -261,10 +312,10 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kernel_class):
-    """HBM bytes per launch of `kernel_class` from the committed rocprofv3 PMC passes
-    (profiles/<round>_traffic.json, made by tools/profile_round.sh + tools/pmc_traffic.py), used only
-    when they were measured on the same kernel sources (sha256 stamp)."""
+def pmc_lookup(kernel_class, workload):
+    """PMC figures of `kernel_class` from the newest committed profiles/*_traffic.json measured on the
+    same kernel sources (sha256 stamp) AND the same workload, averaged over that class's kernel
+    instances weighted by their launches (the class time bench.py reports averages the same launches)."""
     import glob
 
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -273,9 +324,16 @@ def pmc_traffic(kernel_class):
     sha = sources_sha()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("sources_sha") == sha and kernel_class in d.get("kernels", {}):
-            return round(d["kernels"][kernel_class]["hbm_bytes"]), os.path.relpath(f, ROOT)
-    return None, "no PMC traffic measured for these kernel sources (run tools/profile_round.sh)"
+        if d.get("sources_sha") != sha or d.get("workload") != workload:
+            continue
+        inst = [v for v in d.get("kernels", {}).values() if v.get("class") == kernel_class]
+        out = {"source": os.path.relpath(f, ROOT), "instances": [v["kernel"][:80] for v in inst]}
+        for field in ("hbm_bytes", "mfma_util"):
+            vals = [(v[field], v.get("launches", 1)) for v in inst if field in v]
+            if vals:
+                out[field] = round(sum(x * w for x, w in vals) / sum(w for _, w in vals), 4 if field == "mfma_util" else 0)
+        return out
+    return {"source": "no PMC pass on these kernel sources and workload (run tools/profile_round.sh)"}
 
 
 def one_step_mse(sim, mesh, dev, a):
@@ -338,7 +396,8 @@ def cpu_baseline(a, b, lay):
         O.l2_loss(tdn, net, x[:, lay["nti"]]).backward()
         opt.step()
 
-    step()  # warm-up
+    for _ in range(3):  # warm-up (3 warm-up, >= 10 timed, median)
+        step()
     ts = []
     for _ in range(a.cpu_steps):
         t0 = time.perf_counter()
@@ -357,7 +416,7 @@ def cpu_baseline(a, b, lay):
     except OSError:
         pass
     return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": cores, "kind": "port",
-            "sample": "%d timed + 1 warm-up full steps of the same workload (N=%d, E=%d), torch %s fp32, median"
+            "sample": "%d timed + 3 warm-up full steps of the same workload (N=%d, E=%d), torch %s fp32, median"
                       % (a.cpu_steps, b["x"].shape[0], b["edge_index"].shape[1], torch.__version__),
             "cpu": model, "host": platform.node()}
 

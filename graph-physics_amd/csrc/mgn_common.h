@@ -153,7 +153,7 @@ void mgn_set_error(const std::string& s);
 // Kernel classes timed by mgn_profile_* (HIP events on the launch stream; off by default).
 enum MgnProfKind {
     PROF_FWD_EDGE = 0, PROF_FWD_NODE, PROF_FWD_DENSE, PROF_BWD_EDGE, PROF_BWD_NODE, PROF_BWD_DENSE,
-    PROF_WGRAD, PROF_WGRAD_REDUCE, PROF_COMBINE, PROF_PACK, PROF_ADAMW, PROF_PROJ, PROF_KINDS
+    PROF_WGRAD, PROF_WGRAD_REDUCE, PROF_COMBINE, PROF_PACK, PROF_ADAMW, PROF_PROJ, PROF_WGRAD_DENSE, PROF_KINDS
 };
 int mgn_prof_begin(int kind, hipStream_t st);  // returns slot or -1 when disabled
 void mgn_prof_end(int slot, hipStream_t st);

@@ -1661,12 +1661,13 @@ bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
     return true;
 }
 
-int launch_ring(const RgArgs& r, hipStream_t st) {
+// prof_kind: PROF_WGRAD for the processor blocks' launch, PROF_WGRAD_DENSE for encoders / decoder
+int launch_ring(const RgArgs& r, hipStream_t st, int prof_kind = PROF_WGRAD_DENSE) {
     if (int e = set_lds((const void*)wgrad_ring_kernel, RG_LDS)) return e;
     int wgs = 0;
     for (int j = 0; j < r.njobs; ++j) wgs = r.job[j].wg0 + r.job[j].nchunks > wgs ? r.job[j].wg0 + r.job[j].nchunks : wgs;
     if (wgs == 0) return 0;
-    ProfScope ps(PROF_WGRAD, st);
+    ProfScope ps(prof_kind, st);
     hipLaunchKernelGGL(wgrad_ring_kernel, dim3(wgs), dim3(512), RG_LDS, st, r);
     MGN_LAUNCH_CHECK();
     return 0;
@@ -1686,7 +1687,7 @@ int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
     const size_t lds = wgrad_lds_bytes<T, H>(a.gathered != 0);
     if (int e = set_lds((const void*)fn, wgrad_lds_bytes<T, H>(true))) return e;
     if (nchunks > 0 && nj > 0) {
-        ProfScope ps(PROF_WGRAD, st);
+        ProfScope ps(PROF_WGRAD_DENSE, st);
         hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS * WG_GROUPS), lds, st, a);
         MGN_LAUNCH_CHECK();
     }
@@ -1887,7 +1888,7 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
         add(dP + (int64_t)s2 * RPN * H, in.x, H, RPN, in.N, in.epart, Ge, 0, -1, H, edge->in_dim, edge->in_dim,
             (1 + s2) * H, rp, ce);
     r.njobs = nj;
-    if (int e2 = launch_ring(r, st)) return e2;
+    if (int e2 = launch_ring(r, st, PROF_WGRAD)) return e2;
     RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
                     red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
     (void)re;

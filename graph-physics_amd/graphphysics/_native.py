@@ -113,7 +113,7 @@ EXPORTS = {
 }
 
 PROF_KINDS = ["fwd_edge", "fwd_node", "fwd_dense", "bwd_edge", "bwd_node", "bwd_dense", "wgrad",
-              "wgrad_reduce", "combine", "pack", "adamw", "proj"]
+              "wgrad_reduce", "combine", "pack", "adamw", "proj", "wgrad_dense"]
 
 
 def profile_enable(on=True):
@@ -205,7 +205,7 @@ class ErrorWord:
 
     def poll(self):
         ev = self.event
-        if ev is None or not ev.query():
+        if ev is None or torch.cuda.is_current_stream_capturing() or not ev.query():
             return
         self.event = None
         bits = int(self.host[0])
@@ -237,6 +237,8 @@ def error_word(device):
         d = torch.device(d.type, torch.cuda.current_device())
     w = _ERR_WORDS.get(d)
     if w is None:
+        if torch.cuda.is_current_stream_capturing():  # its storage must outlive any graph pool
+            raise RuntimeError("libmgn: run one eager call on this device before capturing a graph")
         w = _ERR_WORDS[d] = ErrorWord(d)
     return w
 

@@ -161,3 +161,25 @@ def plate_sample(seed=0, nx=25, ny=13, nz=4, spacing=0.04):
     nxt[:n_p] += 1e-4 * rng.standard_normal((n_p, 3)) * (nt[:n_p, None] == NORMAL)
     x = np.concatenate([world, nt[:, None]], 1).astype(np.float32)
     return {"x": x, "y": nxt.astype(np.float32), "pos": mesh_pos.astype(np.float32), "cells": cells}
+
+
+def plate_graph(device, seed=0, **kw):
+    """plate_sample() through the reference's DeformingPlate preprocessing on the device
+    (build_preprocessing with world_pos_parameters {0, 3, node_type_index 6}, plate.json:17-37):
+    add_obstacles_next_pos → FaceToEdge (tetrahedra) → world edges (r = 0.03) → Cartesian + Distance
+    → relative world-pos features. Returns (Data with x [N, 7] = [world(3), disp(3), type],
+    y [N, 3], edge_index, edge_attr [E, 8]; the Simulator layout dict)."""
+    import torch
+
+    from graphphysics.dataset.preprocessing import build_preprocessing
+    from graphphysics.utils.data import Data
+
+    s = plate_sample(seed=seed, **kw)
+    d = Data(x=torch.from_numpy(s["x"]).to(device), y=torch.from_numpy(s["y"]).to(device),
+             pos=torch.from_numpy(s["pos"]).to(device),
+             face=torch.from_numpy(s["cells"]).t().contiguous().to(device))
+    g = build_preprocessing(world_pos_parameters={"world_pos_index_start": 0, "world_pos_index_end": 3,
+                                                  "node_type_index": 6})(d)
+    g.face = None
+    lay = dict(node_in=15, edge_in=8, out=3, fs=(0, 6), os=(0, 3), nti=6)
+    return g, lay

@@ -1,0 +1,251 @@
+"""GPU parity of the MGN model on the two single-GPU BASELINE configs beyond CylinderFlow
+(SURVEY.md §8 Cfg C and Cfg E), against the oracle (the reference's ops on the CPU):
+
+  Cfg C  DeformingPlate MGN (reference training_config/plate.json:9-36 with type = epd): a plate-shaped
+         tet mesh + obstacle (meshes.plate_sample, ~1.35k nodes) through the reference's world-pos
+         preprocessing on the device (add_obstacles_next_pos, FaceToEdge, add_world_edges r = 0.03,
+         Cartesian + Distance, world-pos features: preprocessing.py:49-174) -> node_in 6 + 9 = 15,
+         edge_in 8, out 3, MP = 15, h = 128; the whole Simulator training forward + backward.
+  Cfg E  3D aneurysm (reference coarse-aneurysm.json:9-24, torch_graph.py:16-110): the in-tree mock
+         mesh, k-hop 2 built on the device (N = 22,535, E = 1,395,256, max in-degree 103), node_in
+         14 + 9 = 23, edge_in 4, out 3, MP = 15, h = 128.
+
+Tolerances (as tests/test_gpu_parity.py): fp32 forward rel-L2 <= 1e-4 for the full
+15-block model and elementwise <= 1e-5(1 + |ref|) for the preamble; fp32 gradients no further from
+the fp64 evaluation than max(2 x the reference fp32 path's own error, 2e-3 ReLU-tie floor); bf16 no
+further from fp64 than 2 x PyTorch's CPU bf16 autocast of the reference (full model) or rel-L2 <=
+1e-2 forward / 1.5e-1 gradients (single block); the fp32 segmented sum at in-degree 103 bit-exact
+against ATen's scatter_add_ (same visiting order).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    import __graft_entry__ as ge
+
+    ge.build()
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+def relerr(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def assert_vs_truth(got, ref32, ref64, floor=1e-5, tie_tol=2e-3, what=""):
+    e_ref, e_got = relerr(ref32, ref64), relerr(got, ref64)
+    assert e_got <= max(floor, 2 * e_ref, tie_tol), f"{what}: libmgn {e_got:.2e} vs fp64, reference fp32 {e_ref:.2e}"
+
+
+def assert_close_elem(got, ref, tol=1e-5):
+    got, ref = got.detach().double().cpu(), ref.detach().double().cpu()
+    bad = (got - ref).abs() > tol * (1 + ref.abs())
+    assert not bad.any(), f"max err {(got - ref).abs().max().item()}"
+
+
+# ----------------------------------------------------------------------------- Cfg C: DeformingPlate
+@pytest.fixture(scope="module")
+def plate():
+    from graphphysics.utils import meshes
+
+    g, lay = meshes.plate_graph(DEV, seed=0)
+    return g, lay
+
+
+def _oracle_sim(model, lay):
+    return O.OracleSimulator(model, lay["node_in"], lay["edge_in"], lay["out"], feature_slice=lay["fs"],
+                             output_slice=lay["os"], node_type_index=lay["nti"])
+
+
+def _sim(lay, dtype, mp=15, h=128):
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, lay["node_in"], lay["edge_in"], lay["out"], h, compute_dtype=dtype)
+    return Simulator(lay["node_in"], lay["edge_in"], lay["out"], lay["fs"][0], lay["fs"][1], lay["os"][0],
+                     lay["os"][1], lay["nti"], m, DEV)
+
+
+def test_plate_graph_shapes(plate):
+    """Cfg C input contract: node features 6 + one-hot 9, edge_attr 8 (Cartesian 3 + Distance 1 +
+    relative world pos 3 + norm 1), world edges present, edge_index coalesced and symmetric."""
+    from graphphysics.utils import meshes
+
+    g, lay = plate
+    s = meshes.plate_sample(seed=0)
+    n = s["x"].shape[0]
+    assert g.x.shape == (n, 7) and g.y.shape == (n, 3) and g.edge_attr.shape == (g.edge_index.shape[1], 8)
+    ei = g.edge_index.cpu()
+    mesh_only = 0
+    from oracle import graph_oracle as GO
+
+    mesh_only = GO.face_to_edge(torch.from_numpy(s["cells"]).t().contiguous(), n).shape[1]
+    assert ei.shape[1] > mesh_only  # world edges between the obstacle and the plate
+    key = ei[0] * n + ei[1]
+    assert torch.equal(key, key.sort().values) and torch.unique(key).numel() == key.numel()
+    rev = torch.sort(ei[1] * n + ei[0]).values
+    assert torch.equal(rev, key)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_plate_simulator_train_step_vs_oracle(plate, dtype):
+    """Cfg C: Simulator training forward (preamble + 15-block EPD) and backward of the masked L2
+    loss through libmgn vs the oracle on the same preprocessed plate graph."""
+    from graphphysics.utils.loss import masked_mse
+    from graphphysics.utils.nodetype import NodeType
+
+    g, lay = plate
+    sim = _sim(lay, dtype)
+    net, tdn, _ = sim(g)
+    masks = [NodeType.NORMAL, NodeType.OUTFLOW]
+    loss = masked_mse(tdn, net, g.x[:, lay["nti"]], masks)
+    loss.backward()
+    torch.cuda.synchronize()
+
+    torch.manual_seed(0)
+    ref = O.OracleEPD(15, lay["node_in"], lay["edge_in"], lay["out"], 128)
+    osim = _oracle_sim(ref, lay)
+    x, y, ei, ea = g.x.cpu(), g.y.cpu(), g.edge_index.cpu(), g.edge_attr.cpu()
+    # the preamble (target delta, one-hot, three normalizers) against the reference's ops
+    pre = x[:, 0:3]
+    tdn_r = osim.out_norm(y - pre, True)
+    onehot = torch.nn.functional.one_hot(x[:, lay["nti"]].long(), 9)
+    nfn_r = osim.node_norm(torch.cat([x[:, 0:6], onehot], 1), True)
+    ean_r = osim.edge_norm(ea, True)
+    assert_close_elem(tdn, tdn_r)
+    rp = dict(ref.named_parameters())
+    yr = O.encode_process_decode(nfn_r, ei, ean_r, rp, 15)
+    nt = x[:, lay["nti"]]
+    lr = O.l2_loss(tdn_r, yr, nt)
+    lr.backward()
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(nfn_r.double(), ei, ean_r.double(), p64, 15)
+    O.l2_loss(tdn_r.double(), y64, nt).backward()
+    if dtype == torch.float32:
+        assert relerr(net, yr) < 1e-4
+        assert relerr(net, y64) <= max(1e-6, 2 * relerr(yr, y64))
+        assert abs(loss.item() - lr.item()) <= 1e-4 * lr.item()
+        for k, p in sim.model.named_parameters():
+            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, what=k)
+        return
+    pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = O.encode_process_decode(nfn_r, ei, ean_r, pac, 15)
+    O.l2_loss(tdn_r, yac.float(), nt).backward()
+    assert relerr(net, y64) <= 2 * relerr(yac, y64)
+    for k, p in sim.model.named_parameters():
+        assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
+
+
+# ----------------------------------------------------------------------------- Cfg E: aneurysm k-hop 2
+@pytest.fixture(scope="module")
+def aneurysm():
+    from graphphysics.utils import graph_build as G
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "aneurysm_mesh.npz"))
+    pos = torch.from_numpy(z["pos"]).to(DEV)
+    tet = torch.from_numpy(z["tetra"].astype(np.int64)).t().contiguous().to(DEV)
+    n = pos.shape[0]
+    ei = G.k_hop_edge_index(G.face_to_edge(tet, n), 2, n)
+    ea = G.edge_features(pos, ei)
+    rng = np.random.default_rng(1234)
+    feats = rng.standard_normal((n, 14)).astype(np.float32)
+    nt = rng.choice([0, 4, 5, 6], size=n, p=[0.9, 0.01, 0.01, 0.08]).astype(np.float32)
+    x = torch.from_numpy(np.concatenate([feats, nt[:, None]], 1))
+    y = torch.from_numpy((feats[:, 0:3] + 0.01 * rng.standard_normal((n, 3))).astype(np.float32))
+    return n, ei, ea, x, y
+
+
+def test_aneurysm_graph_is_cfg_e(aneurysm):
+    n, ei, ea, x, y = aneurysm
+    assert (n, ei.shape[1]) == (22535, 1395256)
+    deg = torch.bincount(ei[1].cpu(), minlength=n)
+    assert int(deg.max()) == 103 and ea.shape == (1395256, 4)
+
+
+def test_aneurysm_segment_sum_degree_103_bitexact(aneurysm):
+    """fp32 segmented sum over the target-sorted in-edges at in-degree up to 103 (mgn_segment_sum on
+    the block topology) equals ATen's scatter_add_ over edge_index[1] bit for bit: the coalesced
+    (row, col) order visits each target's in-edges in increasing source order, as the CSC order does."""
+    from graphphysics import _native as nat
+    from graphphysics.models import _engine
+
+    n, ei, ea, x, y = aneurysm
+    E = ei.shape[1]
+    topo = _engine.get_topology(ei, n)
+    g = torch.Generator().manual_seed(3)
+    m = torch.randn(E, 128, generator=g)
+    ref = torch.zeros(n, 128).scatter_add_(0, ei[1].cpu()[:, None].expand(-1, 128), m)
+    md = m.to(DEV)
+    msorted = _engine._permute(md, topo.csc_eid, E, 128, nat.MGN_F32, torch.float32, False,
+                               nat.stream_ptr(DEV))
+    out = torch.empty(n, 128, device=DEV)
+    nat.check(nat.lib().mgn_segment_sum(nat.ptr(msorted), nat.ptr(topo.col_ptr), n, 128, nat.MGN_F32,
+                                        nat.ptr(out), nat.stream_ptr(DEV)))
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_aneurysm_block_bf16_chained_degree_103_vs_fp64(aneurysm):
+    """One bf16 h=128 GraphNetBlock on the Cfg E graph: the chained node kernel aggregates 103 in-edges
+    per node in batches (MGN_NODE_AG per round trip); forward and gradients vs the fp64 oracle block
+    on the same bf16-representable inputs (single-block bf16 bounds)."""
+    from graphphysics.models.layers import GraphNetBlock
+
+    n, ei, ea, x, y = aneurysm
+    E = ei.shape[1]
+    g = torch.Generator().manual_seed(5)
+    xb = torch.randn(n, 128, generator=g).bfloat16().float()
+    eb = torch.randn(E, 128, generator=g).bfloat16().float()
+    gx = torch.randn(n, 128, generator=g)
+    ge = torch.randn(E, 128, generator=g)
+    torch.manual_seed(0)
+    blk = GraphNetBlock(128)
+    blk.compute_dtype = torch.bfloat16
+    rp = {k: v.detach().double().requires_grad_(True) for k, v in blk.named_parameters()}
+    blk = blk.to(DEV)
+    xd = xb.to(DEV).requires_grad_(True)
+    ed = eb.to(DEV).requires_grad_(True)
+    x1, e1 = blk(xd, ei, ed)
+    ((x1.float() * gx.to(DEV)).sum() + (e1.float() * ge.to(DEV)).sum()).backward()
+    torch.cuda.synchronize()
+    x64 = xb.double().requires_grad_(True)
+    e64 = eb.double().requires_grad_(True)
+    xr, er = O.graph_net_block(x64, ei.cpu(), e64, rp, "")
+    ((xr * gx.double()).sum() + (er * ge.double()).sum()).backward()
+    assert relerr(x1, xr) <= 1e-2 and relerr(e1, er) <= 1e-2
+    assert relerr(xd.grad, x64.grad) <= 1.5e-1 and relerr(ed.grad, e64.grad) <= 1.5e-1
+    for k, p in blk.named_parameters():
+        assert relerr(p.grad, rp[k].grad) <= 1.5e-1, k
+
+
+def test_aneurysm_simulator_fp32_forward_full_size(aneurysm):
+    """Cfg E at full size, fp32: Simulator training-mode forward (preamble + 15-block EPD) through
+    libmgn vs the oracle — full-model rel-L2 <= 1e-4 and no further from fp64... (fp64 at 4.3 TFLOP is
+    skipped at this size; the fp32 oracle is the reference's own arithmetic)."""
+    from graphphysics.utils.data import Data
+
+    n, ei, ea, x, y = aneurysm
+    lay = dict(node_in=23, edge_in=4, out=3, fs=(0, 14), os=(0, 3), nti=14)
+    sim = _sim(lay, torch.float32)
+    with torch.no_grad():
+        net, tdn, _ = sim(Data(x=x.to(DEV), y=y.to(DEV), edge_index=ei, edge_attr=ea))
+    torch.cuda.synchronize()
+    torch.manual_seed(0)
+    ref = O.OracleEPD(15, 23, 4, 3, 128)
+    osim = _oracle_sim(ref, lay)
+    with torch.no_grad():
+        nr, tr, _ = osim.forward(x, y, ei.cpu(), ea.cpu(), True)
+    assert_close_elem(tdn, tr)
+    assert relerr(net, nr) < 1e-4

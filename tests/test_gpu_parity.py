@@ -477,9 +477,9 @@ def test_invalid_node_type_raises_like_one_hot(bad, msg):
     x = data.x.clone()
     x[7, 2] = bad
     data.x = x
-    with torch.no_grad():
-        sim(data)
-    with pytest.raises(RuntimeError, match=msg):
+    with pytest.raises(RuntimeError, match=msg):  # raised by a later poll in the same forward, or at the check
+        with torch.no_grad():
+            sim(data)
         nat.check_errors(DEV)
     nat.check_errors(DEV)  # cleared
     st = TrainStep(sim, opt, sch, data, graph=True)

@@ -1,13 +1,15 @@
-"""Parse rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-kernel-class HBM bytes per launch.
+"""Parse rocprofv3 PMC passes into per-kernel-INSTANCE figures per launch (medians), stamped with the
+kernel sources' sha256 and the bench workload they were measured on, so bench.py only attaches
+counters of the same kernel instance, build and workload.
 
-Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): counters are in KB (x1024);
-on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads -> doubled.
-WRITE_SIZE is exact for 16-B stores. Output is stamped with the sha256 of the kernel sources so
-bench.py only reports traffic measured on the same build.
-    python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
+  HBM bytes: FETCH_SIZE / WRITE_SIZE passes; counters in KB (x1024); on gfx950 FETCH_SIZE reports
+             half the bytes of wide (16 B/lane) streaming reads -> doubled (MI355X_MICROARCH.md, HBM).
+  MFMA:      SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over SIMDs) and GRBM_GUI_ACTIVE (GPU-busy cycles
+             summed over the 8 XCDs): mfma_util = MFMA_BUSY / (SIMDs x GRBM_GUI_ACTIVE / 8).
+
+    python tools/pmc_traffic.py <workload> <out.json> <fetch.csv> <write.csv> [<sq.csv>]
 """
 import csv
-import glob
 import hashlib
 import json
 import os
@@ -16,61 +18,75 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-
-HOT_SOURCES = ["mgn_common.h", "mgn_chain.h", "mgn_mlp.hip", "mgn_chain.hip", "mgn_chain16.hip", "mgn_graph.hip"]
+HOT_SOURCES = ["mgn_common.h", "mgn_chain.h", "mgn_mlp.hip", "mgn_chain16.hip", "mgn_graph.hip"]
+SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
+XCDS = 8
 
 
 def sources_sha():
+    """sha256 of the training-step kernel sources (graph construction in mgn_build.hip is not in the step)."""
     h = hashlib.sha256()
-    # the training-step kernels only (graph construction in mgn_build.hip does not run in the step)
-    files = [os.path.join(ROOT, "graph-physics_amd", "csrc", f) for f in HOT_SOURCES]
-    for f in files:
-        h.update(open(f, "rb").read())
+    for f in HOT_SOURCES:
+        h.update(open(os.path.join(ROOT, "graph-physics_amd", "csrc", f), "rb").read())
     return h.hexdigest()[:16]
 
 
 def kernel_class(name):
+    """bench.py / libmgn profiler class of a kernel instance (None: not a training-step class)."""
     m = re.search(r"mlp_(fwd|bwd)_kernel.*?Li(\d+)ELi(\d+)ELi(\d)E", name)
     if m:
         return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[m.group(4)]
     for key, cls in (("chain16_node_fwd_kernel", "fwd_node"), ("chain16_node_bwd_kernel", "bwd_node"),
+                     ("chain16_dense_fwd_kernel", "fwd_dense"), ("chain16_dense_bwd_kernel", "bwd_dense"),
                      ("chain16_fwd_kernel", "fwd_edge"), ("chain16_bwd_kernel", "bwd_edge"),
-                     ("chain_fwd_kernel", "fwd_edge"), ("chain_bwd_kernel", "bwd_edge"),
-                     ("mlp_wgrad_kernel", "wgrad"), ("wgrad_ring_kernel", "wgrad"), ("wgrad_reduce_kernel", "wgrad_reduce"),
-                     ("node_grad_kernel", "combine"), ("node_proj_kernel", "proj"),
-                     ("adamw", "adamw"), ("pack_kernel", "pack")):
+                     ("mlp_wgrad_kernel", "wgrad_dense"), ("wgrad_ring_kernel", "wgrad"),
+                     ("wgrad_reduce_kernel", "wgrad_reduce"), ("node_grad_kernel", "combine"),
+                     ("node_proj_kernel", "proj"), ("adamw", "adamw"), ("pack_kernel", "pack")):
         if key in name:
             return cls
     return None
 
 
-def load(path, counter):
+def instance_key(r):
+    return "%s|grid=%s" % (r["Kernel_Name"], r.get("Grid_Size", r.get("Grid_Size_X", "")))
+
+
+def load(path):
+    """{instance: {counter: [values per launch]}}"""
     per = {}
+    if not path or not os.path.exists(path):
+        return per
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
+        if kernel_class(r["Kernel_Name"]) is None:
             continue
-        c = kernel_class(r["Kernel_Name"])
-        if c:
-            per.setdefault((c, r["Kernel_Name"]), []).append(float(r["Counter_Value"]) * 1024.0)
+        per.setdefault(instance_key(r), {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return per
 
 
-def main(fetch_csv, write_csv, out):
-    f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+def main(workload, out, fetch_csv, write_csv, sq_csv=None):
+    f, w, q = load(fetch_csv), load(write_csv), load(sq_csv)
     res = {}
-    for key in f:
-        cls, name = key
-        fb = 2.0 * statistics.median(f[key])
-        wb = statistics.median(w.get(key, [0.0]))
-        if cls in res and "bf16" not in name and "DF16b" not in name:
-            continue  # prefer the bf16 (bench) instantiation
-        res[cls] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb, "launches": len(f[key]),
-                    "kernel": name}
-    json.dump({"sources_sha": sources_sha(), "fetch_correction": 2.0, "unit": "bytes per launch (median)",
-               "kernels": res}, open(out, "w"), indent=1)
-    print(json.dumps({k: round(v["hbm_bytes"] / 1e6, 1) for k, v in res.items()}))
+    for key in sorted(set(f) | set(w) | set(q)):
+        name = key.split("|grid=")[0]
+        d = {"class": kernel_class(name), "kernel": name, "grid": key.split("|grid=")[1]}
+        if key in f and "FETCH_SIZE" in f[key]:
+            d["fetch_bytes"] = 2.0 * 1024.0 * statistics.median(f[key]["FETCH_SIZE"])
+            d["launches"] = len(f[key]["FETCH_SIZE"])
+        if key in w and "WRITE_SIZE" in w[key]:
+            d["write_bytes"] = 1024.0 * statistics.median(w[key]["WRITE_SIZE"])
+        if "fetch_bytes" in d and "write_bytes" in d:
+            d["hbm_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+        for c, v in q.get(key, {}).items():
+            d[c] = statistics.median(v)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("GRBM_GUI_ACTIVE"):
+            d["mfma_util"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * d["GRBM_GUI_ACTIVE"] / XCDS)
+        res[key] = d
+    json.dump({"sources_sha": sources_sha(), "workload": workload, "fetch_correction": 2.0,
+               "unit": "per launch (median over launches)", "kernels": res}, open(out, "w"), indent=1)
+    for k, d in res.items():
+        print(f"{d['class']:12s} {d.get('hbm_bytes', 0) / 1e6:8.1f} MB  mfma_util {d.get('mfma_util', float('nan')):.3f}"
+              f"  {d['kernel'][:60]} grid={d['grid']}")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:])
