@@ -4,7 +4,7 @@
 
 struct ChainFwdArgs {
     const __bf16* e;            // [M][128] edge state, target-sorted
-    const float* proj;          // [N][256] node projections (x·W0bᵀ ‖ x·W0cᵀ)
+    const __bf16* proj;         // [N][256] node projections (x·W0bᵀ + b0 ‖ x·W0cᵀ), bf16
     const int32_t* proj_i;      // dst per edge
     const int32_t* proj_j;      // src per edge
     const __bf16* wpack;        // forward 16x16x32 fragments of the 4 layers
@@ -88,6 +88,8 @@ struct ChainNodeBwdArgs {
 };
 
 bool chain_eligible(const mgn_mlp* m);
+int chain16_edge_backward_parts(int64_t M);
+int chain16_node_backward_parts(int64_t M);
 bool chain_node_eligible(const mgn_mlp* m);  // bf16, 256 -> 128 -> 128, 4 layers, RMSNorm
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
@@ -96,7 +98,7 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
                           float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
 // edge MLP forward / backward: 16x16x32 tiles, 12 waves per workgroup (three per SIMD);
 // nparts: number of dscale partial rows written (the reduction's row count)
-int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
+int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
                          int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,

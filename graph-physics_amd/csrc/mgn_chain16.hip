@@ -19,6 +19,17 @@
 
 #include "mgn_chain.h"
 
+// Diagnostics builds only (-DMGN_ABLATE=bits, results wrong when nonzero; see mgn_mlp.hip): edge
+// forward 1 = P gathers from row 0 (cache-resident), 2 = no P loads, 4 = no weight-staging loads,
+// 8 = no stores of outputs / saves
+#ifndef MGN_ABLATE
+#define MGN_ABLATE 0
+#endif
+#ifndef MGN_DIRECT_ROWS
+#define MGN_DIRECT_ROWS 0
+#endif
+
+
 #ifndef MGN_NODE_AG
 #define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
 #endif
@@ -145,6 +156,10 @@ __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int
         const int tile = c >> 6, lane16 = c & 63;
         const int rt = tile >> 2, ks = tile & 3;
         const int ksl = transposed ? 4 : wks[l];
+        if (MGN_ABLATE & 4) {
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            continue;
+        }
         v[u] = *reinterpret_cast<const u32x4*>(pack + woff[l] + ((int64_t)(rt * ksl + ks) * 64 + lane16) * 8);
     }
 #pragma unroll
@@ -219,6 +234,7 @@ __device__ __forceinline__ void gemm16_st(f4 (&acc)[8], const __bf16* W, int l, 
         }
     };
     auto store = [&](int u) {
+        if (MGN_ABLATE & 8) return;
         if (d.r8) {
             bf16x8 c0, c1;
 #pragma unroll
@@ -296,8 +312,10 @@ __device__ __forceinline__ void store_r8(const f4 (&v)[8], __bf16* scr, __bf16* 
             c1[q] = p[1];
         }
         __bf16* p = dst + (((int64_t)tile * 2 + u) * H + 2 * lane) * 8;
-        *reinterpret_cast<bf16x8*>(p) = c0;
-        *reinterpret_cast<bf16x8*>(p + 8) = c1;
+        if (!(MGN_ABLATE & 8)) {
+            *reinterpret_cast<bf16x8*>(p) = c0;
+            *reinterpret_cast<bf16x8*>(p + 8) = c1;
+        }
         lds_fence();
     }
 }
@@ -306,6 +324,21 @@ __device__ __forceinline__ void store_r8(const f4 (&v)[8], __bf16* scr, __bf16* 
 __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16* dst, int64_t tile, int64_t M,
                                            int lane) {
     const int m = lane & 15;
+#if MGN_DIRECT_ROWS
+    // straight from the accumulator layout: 8 stores of 8 B per lane (each wave instruction writes
+    // 32 contiguous bytes of 16 rows; the rows complete in L2), no LDS round trip or fence
+    (void)scr;
+    const int64_t row = tile * TR + m;
+    if (row < M && !(MGN_ABLATE & 8)) {
+        __bf16* p = dst + row * H + 4 * (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const bf16x4 w = {(__bf16)v[t][0], (__bf16)v[t][1], (__bf16)v[t][2], (__bf16)v[t][3]};
+            *reinterpret_cast<bf16x4*>(p + 16 * t) = w;
+        }
+    }
+    return;
+#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         if ((m >> 3) == u) scr_write(v, scr, lane);
@@ -315,7 +348,7 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
             const int rr = 4 * p + (lane >> 4), c = (lane & 15) * 8;
             const u32x4 w = *reinterpret_cast<const u32x4*>(scr + rr * SLD + c);
             const int64_t row = tile * TR + 8 * u + rr;
-            if (row < M) *reinterpret_cast<u32x4*>(dst + row * H + c) = w;
+            if (row < M && !(MGN_ABLATE & 8)) *reinterpret_cast<u32x4*>(dst + row * H + c) = w;
         }
         lds_fence();
     }
@@ -406,14 +439,17 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     for (; tile < a.ntiles; tile += stride) {
         const In16 in = nxt;
         // node projections of this tile (b0 folded into P_i); the layer-0 GEMM covers their latency
-        f4 pi[8], pj[8];
-        {
-            const float* p0 = a.proj + (int64_t)di * (2 * H) + 4 * g;
-            const float* p1 = a.proj + (int64_t)dj * (2 * H) + H + 4 * g;
+        u32x2 pi[8], pj[8];  // bf16 P_i[dst], P_j[src]: features 16t + 4g .. +3
+        if (MGN_ABLATE & 2) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pi[t] = pj[t] = u32x2{0u, 0u};
+        } else {
+            const __bf16* p0 = a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : di) * (2 * H) + 4 * g;
+            const __bf16* p1 = a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : dj) * (2 * H) + H + 4 * g;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                pi[t] = *reinterpret_cast<const f4*>(p0 + 16 * t);
-                pj[t] = *reinterpret_cast<const f4*>(p1 + 16 * t);
+                pi[t] = *reinterpret_cast<const u32x2*>(p0 + 16 * t);
+                pj[t] = *reinterpret_cast<const u32x2*>(p1 + 16 * t);
             }
         }
         int ndi, ndj;
@@ -435,7 +471,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
             unsigned bits = 0u;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                const f4 b = l == 0 ? pi[t] + pj[t] : *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
+                const f4 b = l == 0 ? bf4(pi[t]) + bf4(pj[t]) : *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float v = fmaxf(acc[t][r] + b[r], 0.f);
@@ -1296,12 +1332,12 @@ int set_lds_once(const void* fn, size_t bytes) {
 
 }  // namespace
 
-int chain16_edge_forward(const mgn_mlp* m, const void* e, const float* proj, const int32_t* pi, const int32_t* pj,
+int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
                          int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st) {
     ChainFwdArgs a;
     memset(&a, 0, sizeof(a));
     a.e = reinterpret_cast<const __bf16*>(e);
-    a.proj = proj;
+    a.proj = reinterpret_cast<const __bf16*>(proj);
     a.proj_i = pi;
     a.proj_j = pj;
     a.wpack = reinterpret_cast<const __bf16*>(m->wpack);
@@ -1360,7 +1396,7 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
                                 : (dout ? chain16_bwd_kernel<false, 8> : chain16_bwd_kernel<true, 8>);
     const size_t lds = lds_bwd(nwk);
     if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
-    const int grid = chain16_grid(a.ntiles, nwk);
+    const int grid = chain16_edge_backward_parts(M);
     *nparts = grid;
     ProfScope ps(PROF_BWD_EDGE, st);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nwk * 64), lds, st, a);
@@ -1368,11 +1404,21 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     return 0;
 }
 
-// node tiles are few (N/16): one workgroup per CU, tiles spread wave-major over all of them
+// node tiles are few (N/16): NODE_SPREAD 1 = one workgroup per CU, tiles spread wave-major over all
+// of them; 0 = ceil(tiles / waves) workgroups, leaving the other CUs to a concurrent launch
+#ifndef MGN_NODE_SPREAD
+#define MGN_NODE_SPREAD 1  // measured: compact (0) fwd 27 -> 37.5 us, bwd 20 -> 23 us at Cfg B
+#endif
 static int node_grid(int64_t ntiles) {
     int cus = chain16_grid((int64_t)1 << 30);
-    return (int)(ntiles < cus ? ntiles : cus);
+    const int64_t want = MGN_NODE_SPREAD ? ntiles : cdiv64(ntiles, NW);
+    return (int)(want < cus ? want : cus);
 }
+
+// dscale partial rows the backward launches write (= their grids): the weight-gradient half of a
+// block backward (mgn_block_backward_wgrad) recomputes them from the sizes
+int chain16_edge_backward_parts(int64_t M) { return M > 0 ? chain16_grid(rows_pad(M) / TR, edge_bwd_waves()) : 0; }
+int chain16_node_backward_parts(int64_t M) { return M > 0 ? node_grid(rows_pad(M) / TR) : 0; }
 
 bool chain_node_eligible(const mgn_mlp* m) {
     return m->dtype == MGN_BF16 && m->hidden == H && m->in_dim == 2 * H && m->out_dim == H && m->n_layers == 4 &&
@@ -1436,7 +1482,7 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = 0;
     if (M == 0) return 0;
     if (int e2 = set_lds_once((const void*)chain16_node_bwd_kernel, LDS_TOTAL)) return e2;
-    const int grid = node_grid(a.ntiles);
+    const int grid = chain16_node_backward_parts(M);
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
     hipLaunchKernelGGL(chain16_node_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);

@@ -2000,9 +2000,10 @@ static int mlp_backward_impl(const mgn_mlp* m, int mode, int64_t M, const MlpIn&
 struct ProjArgs {
     const void* x;      // [N][H] (T)
     const void* w0;     // forward fragments of the edge layer 0 ([H x 3H])
-    float* proj;        // [N][2H]
+    float* proj;        // [N][2H] fp32, or bf16 when out_bf16 (the chained bf16 edge kernels)
     const float* bias0; // optional: b0 folded into the x_i block (the chained edge kernel's layer 0)
     int64_t N;
+    int32_t out_bf16;
     int32_t ldi, kstride;
     int32_t wb[2], off[2], ks0[2], nks[2];  // LDS window / leading zero cols / first k-step / k-steps
 };
@@ -2036,7 +2037,13 @@ __global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
             for (int i = 0; i < G::C::NTW; ++i) {
                 f4 v = g.acc[i][j];
                 if (s == 0 && a.bias0) v += ld4u(a.bias0 + g.n_of(i));
-                *reinterpret_cast<f4*>(a.proj + row * (2 * H) + s * H + g.n_of(i)) = v;
+                const int64_t o = row * (2 * H) + s * H + g.n_of(i);
+                if (a.out_bf16) {
+                    const bf16x4 b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.proj) + o) = b;
+                } else {
+                    *reinterpret_cast<f4*>(a.proj + o) = v;
+                }
             }
         }
     }
@@ -2135,7 +2142,8 @@ void proj_window(int H, int s, int* ks0, int* nks, int* off) {
 }
 
 template <class T, int H>
-int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, const float* bias0, hipStream_t st) {
+int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, const float* bias0, hipStream_t st,
+                bool out_bf16 = false) {
     constexpr int BM = bm_for<T, MODE_NODE>(), KSTEP = Mf<T>::KSTEP;
     ProjArgs a;
     memset(&a, 0, sizeof(a));
@@ -2143,6 +2151,7 @@ int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, cons
     a.w0 = edge->wpack;
     a.proj = proj;
     a.bias0 = bias0;
+    a.out_bf16 = out_bf16;
     a.N = N;
     a.kstride = cdiv(3 * H, KSTEP);
     for (int s = 0; s < 2; ++s) proj_window<T>(H, s + 1, &a.ks0[s], &a.nks[s], &a.off[s]);
@@ -2322,7 +2331,9 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     if (dt == MGN_F32) {
         MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, b0, st)))
     } else {
-        MGN_DISPATCH_H(H, rc = (launch_proj<__bf16, HH>(edge, x, t->num_nodes, proj, b0, st)))
+        // the chained edge kernels gather P as bf16 (half the bytes; P rounded once, like the bf16
+        // layer output the reference's autocast produces)
+        MGN_DISPATCH_H(H, rc = (launch_proj<__bf16, HH>(edge, x, t->num_nodes, proj, b0, st, chain)))
     }
     if (rc) return rc;
     MlpIn ein;
@@ -2386,90 +2397,143 @@ size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* 
     return block_ws_parts(t, edge, node).total;
 }
 
-int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
-                       const mgn_block_saved* saved, const void* dx_out, const void* de_out, void* dx, void* de,
-                       float* edge_grads, float* node_grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
-    if (int r = check_mlp(edge)) return r;
-    if (int r = check_mlp(node)) return r;
-    const BlockWs wl = block_ws_parts(t, edge, node);
-    MGN_REQUIRE(ws_bytes >= wl.total, "block backward workspace too small");
-    MGN_REQUIRE(de_out || t->num_edges == 0 || chain_eligible(edge),
-                "de_out = NULL (zero edge-output gradient) needs the chained bf16 h=128 edge MLP");
-    hipStream_t st = (hipStream_t)stream;
+// The block backward in two halves over one workspace: _data (node-MLP backward, edge-MLP backward,
+// node gradients: dx, de) and _wgrad (weight gradients + fixed-order reduction into the gradient
+// buffers). _wgrad reads only what _data left in `ws` and the forward saves, so the caller may run it
+// on another stream, overlapped with the next block's _data on a second workspace (the hot path:
+// the bandwidth-bound weight-gradient launch fills the CUs the latency-bound node kernels leave idle).
+struct BlockBwdCarve {
+    void *mlp_ws, *dx_part, *d_aggr, *dz0, *dP8;
+    void* ndz;       // chained: node dZ saves (R8)
+    float* ndsp;     // chained: node dscale partials
+    float* npart;    // chained: node slabs
+    void* dz8;       // edge dZ saves (R8)
+    float* dsp;      // edge dscale partials
+    float* part;     // edge slabs
+    bool chained;
+};
+
+static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, void* ws,
+                                     const BlockWs& wl) {
+    BlockBwdCarve c;
+    memset(&c, 0, sizeof(c));
     const int H = edge->hidden, dt = edge->dtype;
     char* w = reinterpret_cast<char*>(ws);
-    void* mlp_ws = w + wl.mlp;
-    void* dx_part = w + wl.dxpart;
-    void* d_aggr = w + wl.daggr;
-    void* dz0 = w + wl.dz0;
-    void* dP8 = w + wl.dP8;
+    c.mlp_ws = w + wl.mlp;
+    c.dx_part = w + wl.dxpart;
+    c.d_aggr = w + wl.daggr;
+    c.dz0 = w + wl.dz0;
+    c.dP8 = w + wl.dP8;
+    c.chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
+    if (c.chained) {
+        const int64_t Nn = t->num_nodes;
+        char* q = w + wl.nmlp;
+        c.ndz = q;
+        q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * 2);
+        c.ndsp = reinterpret_cast<float*>(q);
+        q += align_up((size_t)(rows_pad(Nn) / 16) * node->out_dim * sizeof(float));  // = mlp_bwd_ws carve
+        c.npart = reinterpret_cast<float*>(q);
+    }
+    const int64_t E = t->num_edges;
+    const size_t es = dt == MGN_F32 ? 4 : 2;
+    const int ntiles = (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
+    char* p = reinterpret_cast<char*>(c.mlp_ws);
+    c.dz8 = p;
+    p += align_up((size_t)edge->n_layers * rows_pad(E) * H * es);
+    c.dsp = reinterpret_cast<float*>(p);
+    p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
+    c.part = reinterpret_cast<float*>(p);
+    return c;
+}
+
+static int block_bwd_check(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* de_out,
+                           size_t ws_bytes, BlockWs* wl) {
+    if (int r = check_mlp(edge)) return r;
+    if (int r = check_mlp(node)) return r;
+    *wl = block_ws_parts(t, edge, node);
+    MGN_REQUIRE(ws_bytes >= wl->total, "block backward workspace too small");
+    MGN_REQUIRE(de_out || t->num_edges == 0 || chain_eligible(edge),
+                "de_out = NULL (zero edge-output gradient) needs the chained bf16 h=128 edge MLP");
+    MGN_REQUIRE(wl->nmlp - wl->mlp >= mlp_bwd_ws(edge, t->num_edges), "backward workspace too small");
+    return 0;
+}
+
+int mgn_block_backward_data(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                            const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                            void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                            mgn_stream_t stream) {
+    (void)e;
+    (void)edge_grads;
+    BlockWs wl;
+    if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const int H = edge->hidden, dt = edge->dtype;
+    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl);
 
     // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
-    MlpIn nin;
-    memset(&nin, 0, sizeof(nin));
-    nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
-    nin.seg[1] = SrcSeg{saved->aggr, nullptr, H, H, dt, H, 0};
-    nin.nseg = 2;
-    BwdOut on;
-    memset(&on, 0, sizeof(on));
-    on.mode = MODE_NODE;
-    on.o1 = dx_part;
-    on.o2 = d_aggr;
-    const bool chained = chain_eligible(edge) && chain_node_eligible(node) &&
-                         t->num_nodes > 0 && t->num_edges > 0;
-    void* ndz = nullptr;
-    float* ndsp = nullptr;
-    float* npart = nullptr;
-    int nparts = 0;
-    if (chained) {
+    if (c.chained) {
         // chained data gradients; the node MLP's weight gradients join the block's single ring launch
-        const int64_t Nn = t->num_nodes;
-        MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, Nn), "backward workspace too small");
-        char* q = w + wl.nmlp;
-        ndz = q;
-        q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * 2);
-        ndsp = reinterpret_cast<float*>(q);
-        q += align_up((size_t)(rows_pad(Nn) / 16) * node->out_dim * sizeof(float));  // = mlp_bwd_ws carve
-        npart = reinterpret_cast<float*>(q);
-        if (int r = chain16_node_backward(node, Nn, &saved->node, dx_out, ndz, ndsp, &nparts, dx_part, d_aggr, st))
+        MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, t->num_nodes), "backward workspace too small");
+        int nparts = 0;
+        if (int r = chain16_node_backward(node, t->num_nodes, &saved->node, dx_out, c.ndz, c.ndsp, &nparts, c.dx_part,
+                                          c.d_aggr, st))
             return r;
-    } else if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on,
-                                         node_grads, mlp_ws, wl.nmlp - wl.mlp, st)) {
-        return r;
+    } else {
+        MlpIn nin;
+        memset(&nin, 0, sizeof(nin));
+        nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
+        nin.seg[1] = SrcSeg{saved->aggr, nullptr, H, H, dt, H, 0};
+        nin.nseg = 2;
+        BwdOut on;
+        memset(&on, 0, sizeof(on));
+        on.mode = MODE_NODE;
+        on.o1 = c.dx_part;
+        on.o2 = c.d_aggr;
+        if (int r = mlp_backward_impl(node, MODE_NODE, t->num_nodes, nin, &saved->node, dx_out, dt, H, on, node_grads,
+                                      c.mlp_ws, wl.nmlp - wl.mlp, st))
+            return r;
     }
     // edge MLP data gradients: dY = de_out + d_aggr[dst] -> de = de_out + dZ0·W0a, dZ0 (row-major)
-    const int64_t E = t->num_edges, N = t->num_nodes;
-    MGN_REQUIRE(wl.nmlp - wl.mlp >= mlp_bwd_ws(edge, E), "backward workspace too small");
-    const size_t es = dt == MGN_F32 ? 4 : 2;
-    int ntiles = (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
-    char* p = reinterpret_cast<char*>(mlp_ws);
-    void* dz8 = p;
-    p += align_up((size_t)edge->n_layers * rows_pad(E) * H * es);
-    float* dsp = reinterpret_cast<float*>(p);
-    p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
-    float* part = reinterpret_cast<float*>(p);
+    const int64_t E = t->num_edges;
     BwdOut oe;
     memset(&oe, 0, sizeof(oe));
     oe.mode = MODE_EDGE;
-    oe.gath = d_aggr;
+    oe.gath = c.d_aggr;
     oe.gath_idx = t->csc_dst;
     oe.o1 = de;
-    oe.o2 = dz0;
+    oe.o2 = c.dz0;
     if (chain_eligible(edge)) {
-        auto bwd = chain16_edge_backward;
-        if (int r = bwd(edge, E, &saved->edge, de_out, d_aggr, t->csc_dst, dz8, dsp, &ntiles, de, dz0, st)) return r;
+        int ntiles = 0;
+        if (int r = chain16_edge_backward(edge, E, &saved->edge, de_out, c.d_aggr, t->csc_dst, c.dz8, c.dsp, &ntiles,
+                                          de, c.dz0, st))
+            return r;
     } else if (E > 0) {
-        if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, dz8, dsp, st)) return r;
+        if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, c.dz8, c.dsp, st)) return r;
     }
     // node side: dP = segment sums of dZ0, dx = dx_part + dP_i·W0b + dP_j·W0c
     int rc = 0;
     if (dt == MGN_F32) {
-        MGN_DISPATCH_H(H, rc = (launch_node_grad<float, HH>(edge, t, dz0, dx_part, dP8, dx, st)))
+        MGN_DISPATCH_H(H, rc = (launch_node_grad<float, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st)))
     } else {
-        MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, dz0, dx_part, dP8, dx, st)))
+        MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st)))
     }
-    if (rc) return rc;
-    if (chained) {
+    return rc;
+}
+
+int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                             const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                             void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                             mgn_stream_t stream) {
+    (void)dx_out;
+    (void)dx;
+    (void)de;
+    BlockWs wl;
+    if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const int H = edge->hidden, dt = edge->dtype;
+    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl);
+    const int64_t E = t->num_edges, N = t->num_nodes;
+    if (c.chained) {
         BlockWgradIn in;
         in.E = E;
         in.N = N;
@@ -2477,37 +2541,49 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
         in.x = x;
         in.aggr = saved->aggr;
         in.eact = saved->edge.act;
-        in.edz8 = dz8;
-        in.dz0 = dz0;
-        in.dP8 = dP8;
-        in.edsp = dsp;
-        in.entiles = ntiles;
-        in.epart = part;
+        in.edz8 = c.dz8;
+        in.dz0 = c.dz0;
+        in.dP8 = c.dP8;
+        in.edsp = c.dsp;
+        in.entiles = chain16_edge_backward_parts(E);
+        in.epart = c.part;
         in.egrads = edge_grads;
         in.nact = saved->node.act;
-        in.ndz8 = ndz;
-        in.ndsp = ndsp;
-        in.nntiles = nparts;
-        in.npart = npart;
+        in.ndz8 = c.ndz;
+        in.ndsp = c.ndsp;
+        in.nntiles = chain16_node_backward_parts(N);
+        in.npart = c.npart;
         in.ngrads = node_grads;
         return block_wgrad_ring(edge, node, in, st);
     }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
+    const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
     MlpIn ein;
     memset(&ein, 0, sizeof(ein));
     ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
     ein.nseg = 1;
     int nchunks = 0;
-    if (int r = mlp_wgrad_any(edge, E, saved->edge.act, dz8, dsp, ntiles, part, edge_grads, &ein, 1, &nchunks, false,
-                              st))
+    if (int r = mlp_wgrad_any(edge, E, saved->edge.act, c.dz8, c.dsp, ntiles, c.part, edge_grads, &ein, 1, &nchunks,
+                              false, st))
         return r;
+    int rc = 0;
     if (dt == MGN_F32) {
-        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<float, HH>(edge, N, dP8, x, part, nchunks, st)))
+        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<float, HH>(edge, N, c.dP8, x, c.part, nchunks, st)))
     } else {
-        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<__bf16, HH>(edge, N, dP8, x, part, nchunks, st)))
+        MGN_DISPATCH_H(H, rc = (launch_wgrad_proj<__bf16, HH>(edge, N, c.dP8, x, c.part, nchunks, st)))
     }
     if (rc) return rc;
-    return launch_reduce(edge, part, nchunks, dsp, ntiles, edge_grads, st);
+    return launch_reduce(edge, c.part, nchunks, c.dsp, ntiles, edge_grads, st);
+}
+
+int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
+                       const mgn_block_saved* saved, const void* dx_out, const void* de_out, void* dx, void* de,
+                       float* edge_grads, float* node_grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    if (int r = mgn_block_backward_data(t, edge, node, x, e, saved, dx_out, de_out, dx, de, edge_grads, node_grads,
+                                        ws, ws_bytes, stream))
+        return r;
+    return mgn_block_backward_wgrad(t, edge, node, x, e, saved, dx_out, de_out, dx, de, edge_grads, node_grads, ws,
+                                    ws_bytes, stream);
 }
 
 }  // extern "C"

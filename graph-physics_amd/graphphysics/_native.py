@@ -78,6 +78,12 @@ EXPORTS = {
     "mgn_block_backward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
                                   _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _sz, _vp]),
+    "mgn_block_backward_data": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                       _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _sz, _vp]),
+    "mgn_block_backward_wgrad": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                        _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _sz, _vp]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),

@@ -59,6 +59,19 @@ class GraphTopology:
                                    self.row_ptr.data_ptr(), self.row_perm.data_ptr())
 
 
+# the block backward's weight-gradient halves run on a side stream, overlapped with the next block's
+# data half (set False to serialise them on the current stream, e.g. for A/B timing; same results)
+OVERLAP_WGRAD = False
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 _TOPO_CACHE = []  # [(weakref(edge_index), version, num_nodes, topo)], most recent first
 _TOPO_CACHE_MAX = 8
 
@@ -395,15 +408,42 @@ class EPDFunction(torch.autograd.Function):
         de = None if nb and nat.lib().mgn_block_forward_inference_supported(
             ctypes.byref(bdescs[2 * nb - 2]), ctypes.byref(bdescs[2 * nb - 1])) else \
             torch.zeros((E, H), dtype=tdt, device=dev)
+        L = nat.lib()
+        # Each block: the data half (dx, de) on the current stream; the weight-gradient half on a side
+        # stream, overlapped with the next block's data half (two workspaces alternate; a workspace is
+        # reused only after the side stream has finished with it). Joined before returning.
+        overlap = OVERLAP_WGRAD and nb > 1
+        if overlap:
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            wss = [ws, torch.empty_like(ws)]
+            done = [None, None]
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
             de1 = torch.empty((E, H), dtype=tdt, device=dev)
-            nat.check(nat.lib().mgn_block_backward(
-                ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
-                nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
-                nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
-                ctypes.c_void_p(gp + 4 * boff[2 * b + 1]), nat.ptr(ws), ws.numel(), st))
+            args = (ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
+                    nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
+                    nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
+                    ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
+            if not overlap:
+                nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
+            else:
+                w = wss[b % 2]
+                if done[b % 2] is not None:
+                    main.wait_event(done[b % 2])  # the side stream is done reading this workspace
+                nat.check(L.mgn_block_backward_data(*args, nat.ptr(w), w.numel(), st))
+                ready = torch.cuda.Event()
+                ready.record(main)
+                side.wait_event(ready)
+                nat.check(L.mgn_block_backward_wgrad(*args, nat.ptr(w), w.numel(), nat._vp(side.cuda_stream)))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                done[b % 2] = ev
             dx, de = dx1, de1
+        if overlap:
+            for ev in done:
+                if ev is not None:
+                    main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
         gx = gea = None
         nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         if ctx.only_processor:

@@ -183,6 +183,21 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
                        const void* dx_out, const void* de_out, void* dx, void* de,
                        float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                        mgn_stream_t stream);
+/* The same backward as two calls over one workspace (same arguments): _data writes dx, de (and, for
+ * MLPs outside the chained bf16 h=128 kernels, the node-MLP weight gradients); _wgrad then writes the
+ * weight gradients from what _data left in `ws` plus the forward saves, and may run on another
+ * stream (ordered after _data by the caller) concurrently with the next block's _data on ANOTHER
+ * workspace — the weight-gradient launch overlaps the latency-bound kernels of the next block. */
+int mgn_block_backward_data(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                            const void* x, const void* e, const mgn_block_saved* saved,
+                            const void* dx_out, const void* de_out, void* dx, void* de,
+                            float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                            mgn_stream_t stream);
+int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                             const void* x, const void* e, const mgn_block_saved* saved,
+                             const void* dx_out, const void* de_out, void* dx, void* de,
+                             float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                             mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- primitives */
 /* out[k,:] = in[idx[k],:] (gather), or out[idx[k],:] = in[k,:] when scatter != 0. */
