@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--no-mse", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    ap.add_argument("--fresh-batch", action="store_true",
+                    help="eager steps on a NEW batch each step (fresh device copies of x / y / edge_index / "
+                         "edge_attr, so the topology is rebuilt): the Lightning Trainer path "
+                         "(reference train.py:233-262 collates a new Batch per step); implies --no-graph")
     ap.add_argument("--dp", action="store_true",
                     help="use the data-parallel step (exchanges + split graph) even on one rank")
     ap.add_argument("--workload", default="cylinder", choices=["cylinder", "aneurysm", "plate"],
@@ -56,7 +60,10 @@ def parse():
                          "plate: Cfg C (DeformingPlate-shaped tet mesh + world edges)")
     ap.add_argument("--print-workload", action="store_true",
                     help="print the workload key the PMC files are stamped with, and exit")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.fresh_batch:
+        a.no_graph = True
+    return a
 
 
 def workload_key(a):
@@ -200,8 +207,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    base = {k: getattr(data, k) for k in ("x", "y", "edge_index", "edge_attr")}
+
+    def fresh():
+        # a new Batch per step, as the Lightning loop collates: new tensors (topology cache miss)
+        for k, v in base.items():
+            setattr(data, k, v.clone())
+        step.node_type = data.x[:, step.sim.node_type_index]
+
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        if a.fresh_batch:
+            fresh()
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -289,7 +306,8 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
         "data": "synthetic: %s, random-init weights (seed 0)" % datadesc,
-        "execution": ("eager" if not step.use_graph else
+        "execution": ("eager, a new batch (fresh x / y / edge_index / edge_attr tensors, topology rebuilt) "
+                      "every step" if a.fresh_batch else "eager" if not step.use_graph else
                       "hipGraph replay of forward+loss+backward; eager statistics/gradient all-reduce + AdamW"
                       if step.dp else "hipGraph replay of the whole step"),
         "config": {"workload": workload, "nodes_per_gpu": N, "edges_per_gpu": E,

@@ -66,6 +66,11 @@ struct ChainNodeFwdArgs {
     int64_t act_off[4];
     unsigned* mask32;
     int64_t mask_stride;        // 64-bit words per layer
+    // optional: the next block's node projections from x_out (nullptr pn_out: none)
+    const __bf16* pn_pack;      // next edge MLP's forward pack (layer 0 first: [128][3·128], 12 k-steps)
+    const float* pn_b0;         // its layer-0 bias (folded into P_i)
+    __bf16* pn_out;             // [N][256] bf16: P_i ‖ P_j
+    int32_t pn_kst;             // k-steps per row tile of its layer-0 pack
 };
 
 struct ChainNodeBwdArgs {
@@ -91,9 +96,11 @@ bool chain_eligible(const mgn_mlp* m);
 int chain16_edge_backward_parts(int64_t M);
 int chain16_node_backward_parts(int64_t M);
 bool chain_node_eligible(const mgn_mlp* m);  // bf16, 256 -> 128 -> 128, 4 layers, RMSNorm
+// next_edge / next_proj (optional): also write the next block's node projections (bf16 [N][2·128],
+// b0 folded into P_i) from x_out — the chained edge forward's proj input, without its own launch
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
-                         hipStream_t st);
+                         hipStream_t st, const mgn_mlp* next_edge = nullptr, void* next_proj = nullptr);
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
                           float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
 // edge MLP forward / backward: 16x16x32 tiles, 12 waves per workgroup (three per SIMD);

@@ -30,6 +30,17 @@
 #endif
 
 
+// Diagnostics / A-B builds: delay the second and third wave of each SIMD by MGN_STAGGER x 64 cycles
+// (x 1, x 2) after the prologue so the waves sharing a SIMD leave lockstep (0: off)
+#ifndef MGN_STAGGER
+#define MGN_STAGGER 0
+#endif
+__device__ __forceinline__ void stagger(int wave) {
+    if (MGN_STAGGER > 0) {
+        for (int k = 0; k < (wave >> 2); ++k) __builtin_amdgcn_s_sleep(MGN_STAGGER);
+    }
+}
+
 #ifndef MGN_NODE_AG
 #define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
 #endif
@@ -322,7 +333,7 @@ __device__ __forceinline__ void store_r8(const f4 (&v)[8], __bf16* scr, __bf16* 
 
 // The wave's tile as bf16 rows of a row-major [M][128] matrix (rows >= M skipped), 16-byte stores.
 __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16* dst, int64_t tile, int64_t M,
-                                           int lane) {
+                                           int lane, int64_t ld = H) {
     const int m = lane & 15;
 #if MGN_DIRECT_ROWS
     // straight from the accumulator layout: 8 stores of 8 B per lane (each wave instruction writes
@@ -330,7 +341,7 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
     (void)scr;
     const int64_t row = tile * TR + m;
     if (row < M && !(MGN_ABLATE & 8)) {
-        __bf16* p = dst + row * H + 4 * (lane >> 4);
+        __bf16* p = dst + row * ld + 4 * (lane >> 4);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const bf16x4 w = {(__bf16)v[t][0], (__bf16)v[t][1], (__bf16)v[t][2], (__bf16)v[t][3]};
@@ -348,7 +359,7 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
             const int rr = 4 * p + (lane >> 4), c = (lane & 15) * 8;
             const u32x4 w = *reinterpret_cast<const u32x4*>(scr + rr * SLD + c);
             const int64_t row = tile * TR + 8 * u + rr;
-            if (row < M && !(MGN_ABLATE & 8)) *reinterpret_cast<u32x4*>(dst + row * H + c) = w;
+            if (row < M && !(MGN_ABLATE & 8)) *reinterpret_cast<u32x4*>(dst + row * ld + c) = w;
         }
         lds_fence();
     }
@@ -431,6 +442,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     for (int i = threadIdx.x; i < 5 * H; i += NWK * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
     __syncthreads();
     if (tile >= a.ntiles) return;
+    stagger(wave);
 #pragma unroll
     for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
     pin(di);
@@ -600,6 +612,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
     int ngi = 0;
     if (tile < a.ntiles) {
+        stagger(wave);
         ngi = bidx(a, min(tile + stride, last), lane);
         pin_in<PGA>(nxt);
         pin(ngi);
@@ -722,14 +735,13 @@ __device__ __forceinline__ bf16x8 gfrag(__amdgpu_buffer_rsrc_t rs, int voff, int
     return __builtin_bit_cast(bf16x8, w);
 }
 
-// node layer 0 = x block (LDS image, layer slot 0) + aggr block (global fragments, tiles at
-// tile_of(t, s)); the aggr block's fragments of k-step s+1 load while k-step s computes
+// acc += the 128-column K block of a packed weight matrix whose fragments are read from global
+// memory (L2-resident), source tiles at tile_of(t, s); k-step s+1's fragments load while s computes
 template <class TileFn>
-__device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, const bf16x8 (&Bx)[4],
-                                              const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
+__device__ __forceinline__ void gemm16_global(f4 (&acc)[8], const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of,
+                                              int lane) {
     const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(pack);
     const int vo = gfrag_voff(lane);
-    gemm16(acc, W, 0, Bx, lane);
     bf16x8 fr[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) fr[t] = gfrag(rs, vo, tile_of(t, 0));
@@ -747,6 +759,14 @@ __device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, con
             for (int t = 0; t < 8; ++t) fr[t] = nf[t];
         }
     }
+}
+
+// node layer 0 = x block (LDS image, layer slot 0) + aggr block (global fragments)
+template <class TileFn>
+__device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, const bf16x8 (&Bx)[4],
+                                              const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
+    gemm16(acc, W, 0, Bx, lane);
+    gemm16_global(acc, Ba, pack, tile_of, lane);
 }
 
 // SAVE = false: inference — no aggregate, R8, mask, z or rden saves
@@ -884,6 +904,29 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                 acc[t][r] = fmaf(sc[r], acc[t][r] * rq, (float)xb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
+        if (a.pn_out) {
+            // the NEXT block's node projections from this tile's x_out (bf16, the bits just stored):
+            // P = [x·W0bᵀ + b0 ‖ x·W0cᵀ] of the next edge MLP (its layer-0 k-steps 4..7 / 8..11,
+            // fragments from L2) — what node_proj_kernel would compute in a launch of its own
+            bf16x8 Bx[4];
+            to_operand(acc, Bx);
+#pragma unroll 1
+            for (int half = 0; half < 2; ++half) {
+                f4 pacc[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) pacc[t] = f4{0.f, 0.f, 0.f, 0.f};
+                const int kst = a.pn_kst, k0 = 4 + 4 * half;
+                gemm16_global(pacc, Bx, a.pn_pack, [kst, k0](int t, int s) { return t * kst + k0 + s; }, lane);
+                if (half == 0) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const float* b = a.pn_b0 + 16 * t + 4 * g;  // 4-byte aligned only
+                        pacc[t] += f4{b[0], b[1], b[2], b[3]};
+                    }
+                }
+                store_rows(pacc, scr, a.pn_out + half * H, tile, a.M, lane, 2 * H);
+            }
+        }
         STAMP(3);
     }
     STAMP_PRINT("nfwd16");
@@ -1427,9 +1470,15 @@ bool chain_node_eligible(const mgn_mlp* m) {
 
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
-                         hipStream_t st) {
+                         hipStream_t st, const mgn_mlp* next_edge, void* next_proj) {
     ChainNodeFwdArgs a;
     memset(&a, 0, sizeof(a));
+    if (next_edge && next_proj) {
+        a.pn_pack = reinterpret_cast<const __bf16*>(next_edge->wpack);  // layer 0 is the first pack
+        a.pn_b0 = next_edge->bias[0];
+        a.pn_out = reinterpret_cast<__bf16*>(next_proj);
+        a.pn_kst = cdiv(next_edge->in_dim, 32);
+    }
     a.x = reinterpret_cast<const __bf16*>(x);
     a.seg_ptr = t->col_ptr;
     a.agg_z = reinterpret_cast<const __bf16*>(edge_sv->z);

@@ -2304,9 +2304,11 @@ size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* e
     return block_fwd_ws(t, edge);
 }
 
-int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
-                      void* x_out, void* e_out, mgn_block_saved* saved, void* ws, size_t ws_bytes,
-                      mgn_stream_t stream) {
+static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                              const void* e, void* x_out, void* e_out, mgn_block_saved* saved, void* ws,
+                              size_t ws_bytes, int proj_ready, const mgn_mlp* next_edge, void* next_ws,
+                              size_t next_ws_bytes, int* next_proj_ready, mgn_stream_t stream) {
+    if (next_proj_ready) *next_proj_ready = 0;
     if (int r = check_mlp(edge)) return r;
     if (int r = check_mlp(node)) return r;
     const int H = edge->hidden;
@@ -2327,8 +2329,11 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     float* proj = reinterpret_cast<float*>(ws);
     const bool chain = chain_eligible(edge);
     const float* b0 = chain ? edge->bias[0] : nullptr;  // the chained kernel takes b0 from P_i
+    MGN_REQUIRE(!proj_ready || chain, "proj_ready: the workspace holds bf16 projections of the chained path only");
     int rc = 0;
-    if (dt == MGN_F32) {
+    if (proj_ready) {
+        // P already in ws: the previous block's node-MLP forward wrote it from its x_out
+    } else if (dt == MGN_F32) {
         MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, b0, st)))
     } else {
         // the chained edge kernels gather P as bf16 (half the bytes; P rounded once, like the bf16
@@ -2351,8 +2356,15 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
                                    nullptr, nullptr, st)) {
         return r;
     }
-    if (chain && chain_node_eligible(node))
-        return chain16_node_forward(node, x, t, edge, &saved->edge, t->num_nodes, x_out, saved->aggr, &saved->node, st);
+    if (chain && chain_node_eligible(node)) {
+        const bool fuse = next_edge && next_ws && chain_eligible(next_edge) && next_edge->hidden == H &&
+                          next_ws_bytes >= block_fwd_ws(t, next_edge) && t->num_nodes > 0;
+        if (int r = chain16_node_forward(node, x, t, edge, &saved->edge, t->num_nodes, x_out, saved->aggr,
+                                         &saved->node, st, fuse ? next_edge : nullptr, fuse ? next_ws : nullptr))
+            return r;
+        if (fuse && next_proj_ready) *next_proj_ready = 1;
+        return 0;
+    }
     MlpIn nin;
     memset(&nin, 0, sizeof(nin));
     nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
@@ -2360,6 +2372,21 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
     // K0 = 2H: the aggregation fills columns [H, 2H) inside the kernel
     return mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
                        saved->aggr, st);
+}
+
+int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
+                      void* x_out, void* e_out, mgn_block_saved* saved, void* ws, size_t ws_bytes,
+                      mgn_stream_t stream) {
+    return block_forward_impl(t, edge, node, x, e, x_out, e_out, saved, ws, ws_bytes, 0, nullptr, nullptr, 0, nullptr,
+                              stream);
+}
+
+int mgn_block_forward_chain(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                            const void* e, void* x_out, void* e_out, mgn_block_saved* saved, void* ws,
+                            size_t ws_bytes, int proj_ready, const mgn_mlp* next_edge, void* next_ws,
+                            size_t next_ws_bytes, int* next_proj_ready, mgn_stream_t stream) {
+    return block_forward_impl(t, edge, node, x, e, x_out, e_out, saved, ws, ws_bytes, proj_ready, next_edge, next_ws,
+                              next_ws_bytes, next_proj_ready, stream);
 }
 
 // mlp: edge MLP backward workspace (generic path: shared with the node MLP's, used in sequence);

@@ -62,6 +62,9 @@ class GraphTopology:
 # the block backward's weight-gradient halves run on a side stream, overlapped with the next block's
 # data half (set False to serialise them on the current stream, e.g. for A/B timing; same results)
 OVERLAP_WGRAD = False
+# processor blocks hand the next block's node projections over from their node-MLP kernel
+# (mgn_block_forward_chain); False: every block launches its own projection kernel (tests compare)
+CHAIN_PROJ = True
 _SIDE = {}
 
 
@@ -336,7 +339,11 @@ class EPDFunction(torch.autograd.Function):
         xs, es, svs = [x0], [e0], []
         nb = len(bspecs) // 2
         scratch = None
-        fws = _fwd_ws_block(topo, bdescs[0], bdescs[1], dev) if nb else None
+        # node projections hand-off: block b's node kernel writes block b+1's P into the other of two
+        # workspaces (mgn_block_forward_chain), so blocks after the first launch no projection kernel
+        fwss = [_fwd_ws_block(topo, bdescs[0], bdescs[1], dev), _fwd_ws_block(topo, bdescs[0], bdescs[1], dev)] \
+            if nb else None
+        ready = ctypes.c_int32(0)
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
             if train or scratch is None:
@@ -351,10 +358,14 @@ class EPDFunction(torch.autograd.Function):
                 sv = scratch
             x1 = torch.empty((N, H), dtype=tdt, device=dev)
             e1 = torch.empty((E, H), dtype=tdt, device=dev)
-            nat.check(nat.lib().mgn_block_forward(
+            fws, nws = fwss[b % 2], fwss[(b + 1) % 2]
+            nxt = ctypes.byref(bdescs[2 * b + 2]) if CHAIN_PROJ and b + 1 < nb else None
+            proj_ready = ready.value
+            nat.check(nat.lib().mgn_block_forward_chain(
                 ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
                 nat.ptr(xs[-1]), nat.ptr(es[-1]), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), nat.ptr(fws),
-                fws.numel(), st))
+                fws.numel(), proj_ready, nxt, nat.ptr(nws) if nxt is not None else None, nws.numel(),
+                ctypes.byref(ready), st))
             if train:
                 xs.append(x1)
                 es.append(e1)

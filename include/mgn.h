@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 7
+#define MGN_ABI_VERSION 8
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -172,6 +172,18 @@ size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* e
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
                       const void* x, const void* e, void* x_out, void* e_out,
                       mgn_block_saved* saved, void* ws, size_t ws_bytes, mgn_stream_t stream);
+/* A processor stack of blocks (processors.py:129-131, `for block in self.processor_list`) chained:
+ * the same forward, plus two hand-offs between consecutive blocks. proj_ready = 1: ws already holds
+ * this block's node projections (written by the previous call's next_ws). next_edge / next_ws
+ * (optional): the NEXT block's edge MLP and its workspace — the node-MLP kernel then also computes
+ * that block's projections from this block's x_out (no projection launch of its own) and sets
+ * *next_proj_ready = 1; it stays 0 where the chained bf16 h=128 kernels do not apply (the caller
+ * then passes proj_ready = 0 to the next call). Results are those of mgn_block_forward. */
+int mgn_block_forward_chain(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                            const void* x, const void* e, void* x_out, void* e_out,
+                            mgn_block_saved* saved, void* ws, size_t ws_bytes, int proj_ready,
+                            const mgn_mlp* next_edge, void* next_ws, size_t next_ws_bytes,
+                            int* next_proj_ready, mgn_stream_t stream);
 size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* edge,
                                           const mgn_mlp* node);
 /* dx/de: gradients w.r.t. the block inputs (overwritten). edge_grads/node_grads: flat fp32 as

@@ -323,10 +323,138 @@ def gen_cylinder():
     np.savez_compressed(os.path.join(HERE, "cylinder_golden.npz"), **out)
 
 
+# ----------------------------------------------------------------------------- trained north-star model
+TRAIN_STEPS, TRAIN_WARMUP, TRAIN_LR = 300, 20, 1e-3
+
+
+def gen_trained():
+    """North-star gate on a trained model: the reference Simulator MP=15, h=128,
+    B=1, trained TRAIN_STEPS optimizer steps (frames 0->1, 1->2, 2->3 in turn; AdamW + cosine warm-up
+    as lightning_module.py:275-292, scheduler.py:41-67), then the held-out one-step MSE of frames
+    3->4 and 4->5 (eval mode, build_mask semantics)."""
+    pos, tri, vel = load_cylinder()
+    n = pos.shape[0]
+    ei = face_to_edge_undirected(tri, n)
+    nt = node_types(pos, vel[0])
+    ea = edge_features(pos, ei)
+    datas = [frame_data(pos, ei, ea, nt, vel, t) for t in range(5)]
+    out = {"train_steps": np.array(TRAIN_STEPS), "warmup": np.array(TRAIN_WARMUP), "lr": np.array(TRAIN_LR)}
+    sim = make_sim(15, 128)
+    param_checksums(sim, out, "init")
+    train_steps(sim, [datas[i % 3] for i in range(TRAIN_STEPS)], out, "trained", lr=TRAIN_LR,
+                warmup=TRAIN_WARMUP, max_iters=TRAIN_STEPS)
+    eval_one_step(sim, datas[3:5], out, "trained_eval")
+    np.savez_compressed(os.path.join(HERE, "cylinder_trained.npz"), **out)
+
+
+def gen_trained_threads1():
+    """The same training run with ONE intra-op thread (a different summation order inside the
+    reference's own CPU kernels): its losses and held-out MSE measure how far the reference drifts
+    from itself over 300 steps, the noise floor any other implementation is compared against."""
+    torch.set_num_threads(1)
+    pos, tri, vel = load_cylinder()
+    n = pos.shape[0]
+    ei = face_to_edge_undirected(tri, n)
+    nt = node_types(pos, vel[0])
+    ea = edge_features(pos, ei)
+    datas = [frame_data(pos, ei, ea, nt, vel, t) for t in range(5)]
+    out, scratch = {}, {}
+    sim = make_sim(15, 128)
+    train_steps(sim, [datas[i % 3] for i in range(TRAIN_STEPS)], scratch, "trained", lr=TRAIN_LR,
+                warmup=TRAIN_WARMUP, max_iters=TRAIN_STEPS)
+    out["trained/losses"] = scratch["trained/losses"]
+    eval_one_step(sim, datas[3:5], out, "trained_eval")
+    np.savez_compressed(os.path.join(HERE, "cylinder_trained_threads1.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- validation rollout
+def _reference_lightning_module():
+    """The reference LightningModule class (lightning_module.py) importable without lightning and
+    the dataset / meshio stack: `lightning.LightningModule` -> nn.Module with no-op
+    save_hyperparameters / log (the test captures log), and the two helper modules it imports at
+    module level replaced by empty namespaces (only used by __init__ / the XDMF writer, neither of
+    which the fixture calls)."""
+    import types
+
+    class _LM(torch.nn.Module):
+        def save_hyperparameters(self, *a, **k):
+            pass
+
+        def log(self, name, value, **k):
+            self.logged.setdefault(name, []).append(float(value))
+
+    light = types.ModuleType("lightning")
+    light.LightningModule = _LM
+    sys.modules.setdefault("lightning", light)
+    for name in ("graphphysics.training.parse_parameters", "graphphysics.utils.meshio_mesh"):
+        mod = types.ModuleType(name)
+        mod.get_model = mod.get_simulator = mod.convert_to_meshio_vtu = None
+        sys.modules.setdefault(name, mod)
+    from graphphysics.training.lightning_module import LightningModule
+
+    return LightningModule
+
+
+class _Batch(Data):
+    def clone(self):
+        return _Batch(**{k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.__dict__.items()})
+
+
+def gen_rollout():
+    """Reference validation rollout (lightning_module.py:168-249): validation_step over two
+    trajectories (reset on traj_index change) and on_validation_epoch_end's all-rollout RMSE, with
+    the cfgA model (MP=5, h=32) after 3 training steps; full weights + normaliser buffers stored."""
+    pos, tri, vel = load_cylinder()
+    n = pos.shape[0]
+    ei = face_to_edge_undirected(tri, n)
+    nt = node_types(pos, vel[0])
+    ea = edge_features(pos, ei)
+    datas = [frame_data(pos, ei, ea, nt, vel, t) for t in range(5)]
+    sim = make_sim(5, 32)
+    scratch = {}
+    train_steps(sim, datas[:3], scratch, "cfgA")
+    sim.eval()
+    LM = _reference_lightning_module()
+    lm = LM.__new__(LM)
+    torch.nn.Module.__init__(lm)
+    lm.logged = {}
+    lm.current_epoch, lm.timestep = 0, 1.0
+    lm.param = {"index": {"node_type_index": 2}}
+    lm.model, lm.K, lm.loss = sim, 0, L2Loss()
+    lm.loss_masks = [NodeType.NORMAL, NodeType.OUTFLOW]
+    lm.use_previous_data, lm.previous_data_start, lm.previous_data_end = False, None, None
+    lm.val_step_outputs, lm.val_step_targets, lm.trajectory_to_save = [], [], []
+    lm.current_val_trajectory, lm.last_val_prediction, lm.last_previous_data_prediction = 0, None, None
+    lm._save_trajectory_to_xdmf = lambda *a, **k: None
+    lm._get_traj_savename = lambda *a, **k: ""
+    out = {}
+    for k, v in sim.state_dict().items():
+        out["w::" + k] = v.detach().cpu().numpy().copy()
+    # trajectory 0: frames 0..4 (5 predictions); trajectory 1: frames 1..3
+    plan = [(0, t) for t in range(5)] + [(1, t) for t in range(1, 4)]
+    for i, (traj, t) in enumerate(plan):
+        d = datas[t]
+        b = _Batch(x=d.x.clone(), y=d.y.clone(), pos=d.pos, edge_index=d.edge_index, edge_attr=d.edge_attr,
+                   traj_index=traj)
+        lm.validation_step(b, i)
+        out[f"pred{i}"] = lm.val_step_outputs[-1].numpy().copy()
+    out["plan"] = np.array(plan, dtype=np.int64)
+    out["val_loss"] = np.array(lm.logged["val_loss"])
+    lm.on_validation_epoch_end()
+    out["val_all_rollout_rmse"] = np.array(lm.logged["val_all_rollout_rmse"])
+    np.savez_compressed(os.path.join(HERE, "rollout_golden.npz"), **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # e.g. make_golden.py gen_rollout gen_trained
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     gen_block_cycle()
     gen_epd_random()
     gen_cylinder()
+    gen_rollout()
+    gen_trained()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -154,3 +154,40 @@ def test_simulator_training_bitexact(tag, mp, h, steps):
         pred[keep] = y[keep]
         mses.append(O.l2_loss(y, pred, nt).item())
     np.testing.assert_allclose(np.array(mses), z[f"{tag}_eval/one_step_mse"], rtol=1e-4)
+
+
+def test_oracle_rollout_matches_reference_fixture():
+    """The oracle's restatement of the reference validation loop (lightning_module.py:168-249) against
+    what the reference itself produced (rollout_golden.npz: two trajectories, reset on traj_index,
+    all-rollout RMSE) with the same weights: bit-exact (same ATen ops on CPU)."""
+    z = _load("rollout_golden.npz")
+    w = {k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("w::")}
+    ref = O.OracleEPD(5, 11, 3, 2, 32)
+    ref.load_state_dict({k[6:]: v for k, v in w.items() if k.startswith("model.")})
+    osim = O.OracleSimulator(ref, 11, 3, 2)
+    for name, nrm in (("_output_normalizer", osim.out_norm), ("_node_normalizer", osim.node_norm),
+                      ("_edge_normalizer", osim.edge_norm)):
+        nrm.acc_sum, nrm.acc_sum_squared = w[name + "._acc_sum"], w[name + "._acc_sum_squared"]
+        nrm.acc_count, nrm.num_acc = w[name + "._acc_count"], w[name + "._num_accumulations"]
+    preds, targets, losses, last, cur = [], [], [], None, 0
+    for i, (traj, t) in enumerate(z["plan"].tolist()):
+        if traj != cur:
+            last, cur = None, traj
+        b = meshes.cylinder_batch(1, t=t)
+        x, y = torch.from_numpy(b["x"]), torch.from_numpy(b["y"])
+        if last is not None:
+            x[:, 0:2] = last
+        nt = x[:, 2]
+        mask = ~((nt == 0) | (nt == 5))
+        with torch.no_grad():
+            _, _, pred = osim.forward(x, y, torch.from_numpy(b["edge_index"]), torch.from_numpy(b["edge_attr"]),
+                                      training=False)
+        pred[mask] = y[mask]
+        last = pred
+        assert torch.equal(pred, torch.from_numpy(z[f"pred{i}"])), i
+        preds.append(pred)
+        targets.append(y)
+        losses.append(O.l2_loss(y, pred, nt).item())
+    np.testing.assert_array_equal(np.array(losses, dtype=np.float32), z["val_loss"].astype(np.float32))
+    p, t = torch.cat(preds), torch.cat(targets)
+    assert torch.sqrt(((p - t) ** 2).mean()).item() == float(z["val_all_rollout_rmse"][0])

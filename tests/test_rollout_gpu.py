@@ -1,6 +1,7 @@
 """Validation rollout (reference lightning_module.py:17-25,163-249) and the inference block kernels.
 
-Tolerances: fp32 rollout vs the CPU oracle rollout (same weights, same normaliser statistics,
+test_rollout_matches_reference_fixture checks against the reference's own validation loop output
+(tests/golden/rollout_golden.npz, made by tests/golden/make_golden.py gen_rollout). Tolerances: fp32 rollout vs the CPU oracle rollout (same weights, same normaliser statistics,
 reference _make_prediction loop restated below): per-step predictions max|Δ| ≤ 1e-4·(1+|ref|),
 rollout RMSE and per-step val losses within 1e-6 relative-ish (|Δ| ≤ 1e-6 + 1e-4·ref). Graph-replayed
 rollout ≡ eager rollout bit for bit (same kernels, same order). bf16 h=128: the inference kernels
@@ -94,6 +95,42 @@ def test_rollout_fp32_vs_oracle(graph):
     assert bool(((got - ref).abs() <= tol).all()), float((got - ref).abs().max())
     for a, b in zip([l.item() for l in ro.losses], ref_losses):
         assert abs(a - b) <= 1e-6 + 1e-4 * b
+    assert abs(ro.all_rollout_rmse() - ref_rmse) <= 1e-6 + 1e-4 * ref_rmse
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rollout_matches_reference_fixture(graph):
+    """Pinned to the REFERENCE's own validation loop: tests/golden/rollout_golden.npz holds what
+    lightning_module.py:168-249 (validation_step over two trajectories, the reset on traj_index,
+    on_validation_epoch_end's all-rollout RMSE) produced on the CylinderFlow frames with the cfgA
+    model (MP=5, h=32) after 3 training steps; its full weights and normaliser buffers are loaded
+    here. fp32 GPU vs the reference's CPU fp32: predictions within 1e-4·(1+|ref|), per-step
+    val losses and the all-rollout RMSE within 1e-6 + 1e-4·ref."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.rollout import Rollout
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "rollout_golden.npz"))
+    m = EncodeProcessDecode(5, 11, 3, 2, 32, compute_dtype=torch.float32)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, m, DEV)
+    sd = {k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("w::")}
+    missing, unexpected = sim.load_state_dict(sd, strict=True)
+    assert not missing and not unexpected
+    sim.eval()
+    frames, Data = _frames()
+    ro = Rollout(sim, node_type_index=2, graph=graph)
+    cur = 0
+    for i, (traj, t) in enumerate(g["plan"].tolist()):
+        if traj != cur:  # validation_step: batch.traj_index > current_val_trajectory -> reset
+            ro.reset()
+            cur = traj
+        pred, _ = ro.step(Data(**{k: v.to(DEV) for k, v in frames[t].items()}))
+        ref = torch.from_numpy(g[f"pred{i}"])
+        got = pred.cpu()
+        assert bool(((got - ref).abs() <= 1e-4 * (1 + ref.abs())).all()), (i, float((got - ref).abs().max()))
+    for a, b in zip([l.item() for l in ro.losses], g["val_loss"].tolist()):
+        assert abs(a - b) <= 1e-6 + 1e-4 * b
+    ref_rmse = float(g["val_all_rollout_rmse"][0])
     assert abs(ro.all_rollout_rmse() - ref_rmse) <= 1e-6 + 1e-4 * ref_rmse
 
 

@@ -1,0 +1,106 @@
+"""North-star accuracy gate on a TRAINED model (BASELINE.json: one-step velocity MSE |Δ| ≤ 1e-5).
+
+tests/golden/cylinder_trained.npz (tests/golden/make_golden.py gen_trained) holds what the
+reference's own Simulator (MP=15, h=128, B=1, torch.manual_seed(0) init) reached after 300 training
+steps on the CylinderFlow frames 0->1, 1->2, 2->3 in turn — AdamW(lr 1e-3, wd 1e-4, betas
+(0.9, 0.95)) + CosineWarmupScheduler(warmup 20, max_iters 300), the reference's
+lightning_module.py:111-122 training_step and configure_optimizers (275-292) — and the held-out
+one-step MSE on frames 3->4 and 4->5 (eval mode, build_mask semantics, L2Loss over NORMAL ∪ OUTFLOW).
+
+Here libmgn trains the same model from the same init the same way — the eager per-batch path the
+Lightning Trainer drives (a new Batch every step), TrainStep(graph=False) — and must reach the
+same held-out MSE within the reference's own run-to-run noise (bounds in the test docstring).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    import __graft_entry__ as ge
+
+    ge.build()
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+def _train(dtype, z):
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.optim import FusedAdamW
+    from graphphysics.training.step import TrainStep
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+    from graphphysics.utils.scheduler import CosineWarmupScheduler
+
+    steps, warmup, lr = int(z["train_steps"]), int(z["warmup"]), float(z["lr"])
+    torch.manual_seed(0)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, EncodeProcessDecode(15, 11, 3, 2, 128, compute_dtype=dtype), DEV)
+    for k, v in sim.state_dict().items():  # same init as the reference (RNG order)
+        if ("init::" + k) in z:
+            assert abs(v.double().sum().item() - float(z["init::" + k])) <= 1e-6 * (1 + abs(float(z["init::" + k])))
+    opt = FusedAdamW(sim.parameters(), lr=lr, weight_decay=1e-4, betas=(0.9, 0.95))
+    sch = CosineWarmupScheduler(opt, warmup=warmup, max_iters=steps)
+    frames = []
+    for t in range(3):
+        b = meshes.cylinder_batch(1, t=t)
+        frames.append(Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")}))
+    sts = [TrainStep(sim, opt, sch, f, graph=False) for f in frames]
+    losses = torch.stack([sts[i % 3]().detach() for i in range(steps)]).cpu().numpy()
+    sim.eval()
+    mses = []
+    for t in (3, 4):
+        b = meshes.cylinder_batch(1, t=t)
+        x, y = torch.from_numpy(b["x"]), torch.from_numpy(b["y"])
+        d = Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})
+        with torch.no_grad():
+            _, _, pred = sim(d)
+        pred = pred.float().cpu()
+        keep = ~((x[:, 2] == 0) | (x[:, 2] == 5))
+        pred[keep] = y[keep]
+        mses.append(O.l2_loss(y, pred, x[:, 2]).item())
+    return losses, np.array(mses), sim
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_trained_one_step_mse_matches_reference(dtype):
+    """Training is chaotic: the reference run with ONE intra-op thread instead of eight
+    (cylinder_trained_threads1.npz) already drifts from itself — losses 1e-2 apart by step 8, 8 %
+    median over the 300 steps, held-out MSE 3.2e-5 / 3.5e-5 apart (the north-star 1e-5 bound holds
+    only for the same weights, test_gpu_parity.py::test_one_step_mse_matches_reference_path). So
+    libmgn must (1) reproduce the first 3 steps (fp32: 1e-4 relative, before the drift; bf16: 2e-2),
+    (2) stay within the reference's own noise band at the end: |ΔMSE| ≤ max(1e-5, 1.5 × the
+    reference's self-difference) per held-out frame for fp32, 3 × for bf16 (a different rounding
+    trajectory), and (3) train as well: loss curve medians within 10 % (fp32) / 20 % (bf16)."""
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    z = np.load(os.path.join(here, "cylinder_trained.npz"))
+    z1 = np.load(os.path.join(here, "cylinder_trained_threads1.npz"))
+    losses, mses, sim = _train(dtype, z)
+    ref_losses, ref_mses = z["trained/losses"], z["trained_eval/one_step_mse"]
+    noise = np.abs(z1["trained_eval/one_step_mse"] - ref_mses)
+    dl = np.abs(losses - ref_losses) / np.abs(ref_losses)
+    print(f"\n{dtype}: one-step MSE libmgn {mses} reference {ref_mses} |d| {np.abs(mses - ref_mses)} "
+          f"(reference 8 vs 1 threads: {noise}); loss rel diff first 10 {np.array2string(dl[:10], precision=2)}, "
+          f"median {np.median(dl):.2e}, max {dl.max():.2e}")
+    fp32 = dtype == torch.float32
+    np.testing.assert_allclose(losses[:3], ref_losses[:3], rtol=1e-4 if fp32 else 2e-2)
+    assert np.median(dl) <= (0.1 if fp32 else 0.2)
+    bound = np.maximum(1e-5, (1.5 if fp32 else 3.0) * noise)
+    assert np.all(np.abs(mses - ref_mses) <= bound), (mses, ref_mses, bound)
+    # normaliser accumulators after 300 training forwards: the same statistics (the means — the
+    # sums of the near-zero-mean target deltas are cancellation-dominated, fp32 order-sensitive)
+    for name in ("_output_normalizer", "_node_normalizer", "_edge_normalizer"):
+        nrm = getattr(sim, name)
+        cnt = float(z[f"trained/{name}/acc_count"])
+        assert float(nrm._acc_count) == cnt
+        np.testing.assert_allclose(nrm._acc_sum.cpu().double().numpy() / cnt, z[f"trained/{name}/acc_sum"] / cnt,
+                                   rtol=1e-5, atol=1e-8)
+        np.testing.assert_allclose(nrm._acc_sum_squared.cpu().double().numpy() / cnt,
+                                   z[f"trained/{name}/acc_sum_squared"] / cnt, rtol=1e-5, atol=1e-8)
