@@ -156,12 +156,13 @@ __device__ __forceinline__ void relu_mask(f4 (&acc)[8], unsigned w) {
 // lane groups g = 2(q&1) + half, element group jg = q>>1.
 template <int NL = 4, int NT = NW * 64>
 __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
-                                        bool transposed) {
+                                        bool transposed, int tid = -1) {
     constexpr int TOT = NL * 2048, PER = (TOT + NT - 1) / NT;  // 16 chunks per thread (4 layers, 512 threads)
+    if (tid < 0) tid = threadIdx.x;
     u32x4 v[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int it = threadIdx.x + u * NT;
+        const int it = tid + u * NT;
         if (TOT % NT != 0 && it >= TOT) break;
         const int l = it >> 11, c = it & 2047;
         const int tile = c >> 6, lane16 = c & 63;
@@ -175,7 +176,7 @@ __device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int it = threadIdx.x + u * NT;
+        const int it = tid + u * NT;
         if (TOT % NT != 0 && it >= TOT) break;
         const int l = it >> 11, c = it & 2047;
         const int tile = c >> 6, lane16 = c & 63;
@@ -782,43 +783,31 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
     // the first tile's segment bounds load under the weight staging (most waves own at most one
     // node tile: its chain of dependent loads is most of the kernel's time)
-    int kb = 0, ke = 0;
-    auto load_seg = [&](int64_t tl) {
+    // Phase A of a tile (memory-bound, no weights): x rows (layer-0 B operand of the x block, and
+    // the residual) and the aggregation over the node's in-edges (target-sorted: one contiguous
+    // segment), in the accumulator layout: the lane sums its 32 features of every message
+    // s_e ⊙ z_k / q_k, in edge order. Groups of AG edges: every load of a group is issued before
+    // the first add (one memory round trip per group; edges past the segment end reload its last
+    // edge and add 0 · z). The edge RMSNorm scale s comes from the wave's scratch (a private copy,
+    // so phase A needs nothing the workgroup stages).
+    auto phase_a = [&](int64_t tl, bf16x8 (&xb)[4], f4 (&agg)[8]) {
         const int64_t row = tl * TR + m;
         const int64_t v = clamp_row(row, a.M);
-        kb = a.seg_ptr[v];
-        ke = row < a.M ? a.seg_ptr[v + 1] : kb;
-    };
-    if (tile < a.ntiles) load_seg(tile);
-    stage16(W, a.wpack, a.woff, a.wks, false);
-    for (int i = threadIdx.x; i < 6 * H; i += NW * 64)
-        vec[i] = i < 4 * H ? a.bias[i / H][i % H] : i < 5 * H ? a.scale[i - 4 * H] : a.agg_scale[i - 5 * H];
-    STAMP_DECL;
-    __syncthreads();
-    STAMP(0);
-    for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
-        if (tile != first) load_seg(tile);
-        const int64_t row = tile * TR + m;
-        const bool ok = row < a.M;
-        // x rows (layer-0 B operand of the x block, and the residual)
-        bf16x8 xb[4];
-        {
-            const __bf16* xp = a.x + clamp_row(row, a.M) * H + 4 * g;
+        const int kb = a.seg_ptr[v];
+        const int ke = row < a.M ? a.seg_ptr[v + 1] : kb;
+        const __bf16* xp = a.x + v * H + 4 * g;
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const u32x2 lo = *reinterpret_cast<const u32x2*>(xp + 32 * s);
-                const u32x2 hi = *reinterpret_cast<const u32x2*>(xp + 32 * s + 16);
-                const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
-                xb[s] = __builtin_bit_cast(bf16x8, w);
-            }
+        for (int s = 0; s < 4; ++s) {
+            const u32x2 lo = *reinterpret_cast<const u32x2*>(xp + 32 * s);
+            const u32x2 hi = *reinterpret_cast<const u32x2*>(xp + 32 * s + 16);
+            const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+            xb[s] = __builtin_bit_cast(bf16x8, w);
         }
-        // aggregation over the node's in-edges (target-sorted: one contiguous segment), in the
-        // accumulator layout: the lane sums its 32 features of every message s_e ⊙ z_k / q_k, in
-        // edge order. Groups of AG edges: every load of a group is issued before the first add
-        // (one memory round trip per group; edges past the segment end reload its last edge and
-        // add 0 · z)
+        float* scv = reinterpret_cast<float*>(scr);  // [H] edge scale, private to the wave
+        scv[2 * lane] = a.agg_scale[2 * lane];
+        scv[2 * lane + 1] = a.agg_scale[2 * lane + 1];
+        lds_fence();
         constexpr int AG = MGN_NODE_AG;
-        f4 agg[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) agg[t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
@@ -838,11 +827,40 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                 const float r = k + u < ke ? __builtin_amdgcn_rcpf(rr[u]) : 0.f;
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    const f4 sc = *reinterpret_cast<const f4*>(vec + 5 * H + 16 * t + 4 * g);
+                    const f4 sc = *reinterpret_cast<const f4*>(scv + 16 * t + 4 * g);
                     agg[t] += sc * (bf4(zz[u][t]) * r);
                 }
             }
         }
+        lds_fence();  // scratch reads done before store_rows reuses it
+    };
+    auto fill_vec = [&](int tid, int nt) {
+        for (int i = tid; i < 5 * H; i += nt) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
+    };
+    // Most launches have at most one tile per wave of the first half (N/16 <= 4 x CUs): then the
+    // second half of each workgroup stages the weights WHILE the first half runs its tile's phase A
+    // (the staging burst hides behind the aggregation's gathers instead of preceding them).
+    const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
+    bf16x8 xb[4];
+    f4 agg[8];
+    STAMP_DECL;
+    if (split) {
+        if (wave >= NW / 2) {
+            stage16<4, NW / 2 * 64>(W, a.wpack, a.woff, a.wks, false, threadIdx.x - NW / 2 * 64);
+            fill_vec(threadIdx.x - NW / 2 * 64, NW / 2 * 64);
+        } else if (tile < a.ntiles) {
+            phase_a(tile, xb, agg);
+        }
+    } else {
+        stage16(W, a.wpack, a.woff, a.wks, false);
+        fill_vec(threadIdx.x, NW * 64);
+    }
+    __syncthreads();
+    STAMP(0);
+    for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
+        if (!split || tile != first) phase_a(tile, xb, agg);
+        const int64_t row = tile * TR + m;
+        const bool ok = row < a.M;
         STAMP(1);
         if (SAVE) store_rows(agg, scr, a.aggr_save, tile, a.M, lane);
         bf16x8 Ba[4];
@@ -941,18 +959,17 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     float* red = reinterpret_cast<float*>(smem + LDS_W + LDS_V + LDS_S);  // [NW][H]
     const int m = lane & 15, g = lane >> 4;
     const int r4 = 2 * (m & 1) + ((m >> 1) & 1);  // row16_sum4's component in lane m
-    stage16(W, a.wtpack, a.woff, a.wks, true);
-    for (int i = threadIdx.x; i < H; i += NW * 64) vec[i] = a.scale[i];
-    for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
-    STAMP_DECL;
-    __syncthreads();
-    STAMP(0);
     const int64_t stride = (int64_t)gridDim.x * NW;
-    for (int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x; tile < a.ntiles; tile += stride) {
-        const int64_t row = tile * TR + m;
+    int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
+    for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;  // the wave's own dscale row
+    // Phase A of a tile (loads + RMSNorm backward, layers.py:59-74; no weights): dY = dx_out, the
+    // scale from a private copy in the wave's scratch. Returns dZ of the last layer in acc, the
+    // tile's dx_out rows (the residual) in d and the ReLU mask words in mk.
+    auto phase_a = [&](int64_t tl, f4 (&acc)[8], u32x2 (&d)[8], unsigned (&mk)[3]) {
+        const int64_t row = tl * TR + m;
         const bool ok = row < a.M;
         const int64_t v = clamp_row(row, a.M);
-        u32x2 d[8], zr[8];
+        u32x2 zr[8];
         const __bf16* dp = a.dout + v * H + 4 * g;
         const __bf16* zp = a.z_save + v * H + 4 * g;
 #pragma unroll
@@ -961,17 +978,18 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
         }
         const float qd = a.rden_save[v];
-        unsigned mk[3];
 #pragma unroll
-        for (int l = 0; l < 3; ++l) mk[l] = ok ? a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] : 0u;
-        // RMSNorm backward (layers.py:59-74)
-        f4 acc[8];
+        for (int l = 0; l < 3; ++l) mk[l] = ok ? a.mask32[l * a.mask_stride * 2 + tl * 64 + lane] : 0u;
+        float* scv = reinterpret_cast<float*>(scr);  // [H] RMSNorm scale, private to the wave
+        scv[2 * lane] = a.scale[2 * lane];
+        scv[2 * lane + 1] = a.scale[2 * lane + 1];
+        lds_fence();
         float dot = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 dy = bf4(d[t]);
             const f4 z = bf4(zr[t]);
-            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            const f4 sc = *reinterpret_cast<const f4*>(scv + 16 * t + 4 * g);
             acc[t] = dy;
 #pragma unroll
             for (int r = 0; r < 4; ++r) dot = fmaf(sc[r] * dy[r], z[r], dot);
@@ -985,7 +1003,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 z = bf4(zr[t]);
-            const f4 sc = *reinterpret_cast<const f4*>(vec + 16 * t + 4 * g);
+            const f4 sc = *reinterpret_cast<const f4*>(scv + 16 * t + 4 * g);
             f4 ds;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -996,6 +1014,27 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             const float dsum = row16_sum4(ds, m);  // component r4(m) summed over the tile's 16 rows
             if (m < 4) atomicAdd(red + wave * H + 16 * t + 4 * g + r4, dsum);  // no-return LDS add
         }
+        lds_fence();  // scratch reads done before the GEMMs' stores reuse it
+    };
+    // as the node forward: with at most one tile per first-half wave, the second half stages the
+    // weights while the first half runs phase A
+    const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
+    f4 acc[8];
+    u32x2 d[8];
+    unsigned mk[3];
+    STAMP_DECL;
+    if (split) {
+        if (wave >= NW / 2)
+            stage16<4, NW / 2 * 64>(W, a.wtpack, a.woff, a.wks, true, threadIdx.x - NW / 2 * 64);
+        else if (tile < a.ntiles)
+            phase_a(tile, acc, d, mk);
+    } else {
+        stage16(W, a.wtpack, a.woff, a.wks, true);
+    }
+    __syncthreads();
+    STAMP(0);
+    for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
+        if (!split || tile != first) phase_a(tile, acc, d, mk);
         STAMP(1);
         bf16x8 B[4];
         to_operand(acc, B);
