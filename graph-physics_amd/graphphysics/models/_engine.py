@@ -62,6 +62,19 @@ class GraphTopology:
 # the block backward's weight-gradient halves run on a side stream, overlapped with the next block's
 # data half (set False to serialise them on the current stream, e.g. for A/B timing; same results)
 OVERLAP_WGRAD = False
+# Gradient-ready callback (data parallelism): EncodeProcessDecode's backward calls
+# GRAD_READY(G, lo, hi) on the current stream as soon as the flat-gradient range [lo, hi) is final —
+# the decoder's, then each processor block's (last block first), then the encoders' — so a
+# bucketed all-reduce can start while the earlier blocks' backward still runs
+# (graphphysics.training.distributed.GradBuckets). None: no callbacks.
+GRAD_READY = None
+
+
+def _grad_ready(G, lo, hi):
+    if GRAD_READY is not None and hi > lo:
+        GRAD_READY(G, lo, hi)
+
+
 # processor blocks hand the next block's node projections over from their node-MLP kernel
 # (mgn_block_forward_chain); False: every block launches its own projection kernel (tests compare)
 CHAIN_PROJ = True
@@ -293,6 +306,11 @@ def _ws_bytes_block(topo, de, dn):
                                                             ctypes.byref(de), ctypes.byref(dn)))
 
 
+def bspecs_numel(plan, only_processor, i):
+    """Parameter count of processor spec i (block b: edge MLP 2b, node MLP 2b + 1)."""
+    return plan.specs[i if only_processor else 3 + i].numel
+
+
 def _fwd_ws_block(topo, de, dn, dev):
     """Scratch for mgn_block_forward (node projections of the edge MLP's layer 0)."""
     n = int(nat.lib().mgn_block_forward_workspace_bytes(ctypes.byref(topo.struct), ctypes.byref(de),
@@ -413,6 +431,7 @@ class EPDFunction(torch.autograd.Function):
             g = gout.detach().float().contiguous()
             _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                      ctypes.c_void_p(gp + 4 * off[2]), ws, st)
+            _grad_ready(G, off[2], off[2] + plan.specs[2].numel)
         nb = len(bdescs) // 2
         # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
         # gradient is zero, which the chained bf16 kernels take as NULL (no zero fill, no reads)
@@ -438,6 +457,7 @@ class EPDFunction(torch.autograd.Function):
                     ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
             if not overlap:
                 nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
+                _grad_ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
             else:
                 w = wss[b % 2]
                 if done[b % 2] is not None:
@@ -473,6 +493,7 @@ class EPDFunction(torch.autograd.Function):
             gx = gxc
             if nea:
                 gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
+            _grad_ready(G, off[0], off[1] + plan.specs[1].numel)
         ctx.state = None
         return (None, None, None, gx, gea, None, *plan.grad_views(G))
 

@@ -65,3 +65,53 @@ def allreduce_gradients(params, group=None, op=None):
     for g in gs:
         g.copy_(buf[o:o + g.numel()].view_as(g))
         o += g.numel()
+
+
+class GradBuckets:
+    """Bucketed gradient all-reduce overlapped with the backward ("bucket it and
+    overlap it with the backward of later blocks"). Installed as graphphysics.models._engine.GRAD_READY
+    while the step's backward is recorded: each call hands over a flat-gradient range that is final
+    on the compute stream; adjacent ranges (the processor blocks arrive last-first, each right below
+    the previous one) merge into one bucket until it holds `bucket_bytes`, then the bucket is
+    SUM-all-reduced in place on a communication stream that waits only for the work that produced
+    it. finish() flushes the last bucket and joins the communication stream back into the compute
+    stream. Every rank issues the same buckets in the same order (the backward is deterministic), as
+    RCCL requires. Inside a hipGraph capture the collectives are recorded into the graph: one replay
+    then covers forward, backward, the overlapped all-reduces and the optimizer."""
+
+    def __init__(self, group=None, bucket_bytes=4 << 20):
+        self.group = group
+        self.bucket = int(bucket_bytes)
+        self.comm = None
+        self.cur = None  # (G, lo, hi)
+        self.issued = 0
+        self.covered = 0  # elements handed over (TrainStep checks they are the whole buffer)
+
+    def __call__(self, G, lo, hi):
+        self.covered += hi - lo
+        if self.cur is not None and self.cur[0] is G and hi == self.cur[1] \
+                and (self.cur[2] - lo) * G.element_size() <= self.bucket:
+            self.cur = (G, lo, self.cur[2])
+        else:
+            self._flush()
+            self.cur = (G, lo, hi)
+        if (self.cur[2] - self.cur[1]) * G.element_size() >= self.bucket:
+            self._flush()
+
+    def _flush(self):
+        if self.cur is None:
+            return
+        G, lo, hi = self.cur
+        self.cur = None
+        cur = torch.cuda.current_stream(G.device)
+        if self.comm is None:
+            self.comm = torch.cuda.Stream(device=G.device)
+        self.comm.wait_stream(cur)
+        with torch.cuda.stream(self.comm):
+            dist.all_reduce(G[lo:hi], group=self.group)
+        self.issued += 1
+
+    def finish(self):
+        self._flush()
+        if self.comm is not None:
+            torch.cuda.current_stream(self.comm.device).wait_stream(self.comm)

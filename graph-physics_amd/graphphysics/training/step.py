@@ -13,8 +13,12 @@ Data parallel (process group of >1 rank), captured: the three exchanges of
 graphphysics.training.distributed stay outside the graph — the normalizer batch statistics depend
 only on the batch, so Simulator.exchange_statistics() sums them over ranks (one packed all-reduce)
 before the replay; the global masked-node count is fixed per batch; the replay covers forward,
-loss and backward; then ONE all-reduce of the flat gradient buffer and the AdamW launch.
-`graph=False`: the same exchanges, fully eager.
+loss and backward; then ONE all-reduce of the flat gradient buffer and the AdamW launch. Over RCCL
+(backend "nccl") the gradient all-reduce is instead bucketed and overlapped with the backward inside
+the graph (distributed.GradBuckets: the decoder's and each block's gradients are all-reduced on a
+communication stream as soon as the backward has produced them), and AdamW is recorded too: one
+replay per step after the statistics exchange. MGN_GRAD_OVERLAP=0 keeps the all-reduce after the
+replay. `graph=False`: the same exchanges, fully eager.
 
 capture() warms the allocator and the library up with `warmup` eager steps and then RESTORES every
 piece of state they touched (parameters, optimizer moments and step count, scheduler, learning rate,
@@ -24,11 +28,13 @@ eager() or zero_grad() moved it). Validation errors flagged on libmgn's device e
 outside the one-hot range) surface as the reference's RuntimeError at most one step late, without a
 host synchronisation per step.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from graphphysics import _native as nat
-from graphphysics.training.distributed import allreduce_gradients, flat_grad_buffer, global_mask_count
+from graphphysics.training.distributed import GradBuckets, allreduce_gradients, flat_grad_buffer, global_mask_count
 from graphphysics.utils.loss import masked_mse
 from graphphysics.utils.nodetype import NodeType
 
@@ -50,6 +56,13 @@ class TrainStep:
         self._count = None
         self._graph_grads = None  # p.grad views of the captured step's flat gradient buffer
         self._gflat = None
+        # bucketed all-reduce overlapped with the backward, recorded in the graph (RCCL only: gloo
+        # collectives run on the host and cannot be captured)
+        self.overlap = False
+        if self.dp and graph and os.environ.get("MGN_GRAD_OVERLAP", "1") != "0" and dist.is_available() \
+                and dist.is_initialized():
+            self.overlap = dist.get_backend(group) == "nccl"
+        self.buckets = None
         if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
 
@@ -133,9 +146,27 @@ class TrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._loss()
-            loss.backward(self._seed(loss))
-            if not self.dp:
+            if self.overlap:
+                from graphphysics.models import _engine
+
+                mb = float(os.environ.get("MGN_GRAD_BUCKET_MB", "4"))
+                self.buckets = GradBuckets(self.group, bucket_bytes=int(mb * (1 << 20)))
+                _engine.GRAD_READY = self.buckets
+                try:
+                    loss.backward(self._seed(loss))
+                finally:
+                    _engine.GRAD_READY = None
+                self.buckets.finish()
+                total = sum(p.numel() for p in self.params)
+                if self.buckets.covered != total:
+                    raise RuntimeError("overlapped gradient all-reduce covered %d of %d gradient elements (the "
+                                       "model is not one EncodeProcessDecode): set MGN_GRAD_OVERLAP=0"
+                                       % (self.buckets.covered, total))
                 self.opt.launch()
+            else:
+                loss.backward(self._seed(loss))
+                if not self.dp:
+                    self.opt.launch()
         self.graph, self.static_loss = g, loss
         self._graph_grads = [p.grad for p in self.params]
         self._gflat = flat_grad_buffer(self.params)
@@ -157,7 +188,10 @@ class TrainStep:
             self.capture()
         self._bind_graph_grads()
         self.opt.stage()
-        if self.dp:
+        if self.dp and self.overlap:
+            self._prologue()
+            self.graph.replay()  # backward-overlapped gradient all-reduce + AdamW inside
+        elif self.dp:
             self._prologue()
             self.graph.replay()
             if self._gflat is not None and dist.is_available() and dist.is_initialized():

@@ -118,3 +118,47 @@ def test_two_rank_libmgn_captured_step_equals_single_process(dtype, mp_, h):
     for b0, b1, bb in zip(r[0]["bufs"], r[1]["bufs"], bufs):  # normaliser accumulators: global stats
         torch.testing.assert_close(b0, b1, rtol=0, atol=0)
         torch.testing.assert_close(b0, bb, rtol=1e-5, atol=1e-5)
+
+
+def _worker_rccl(rank, world, port, out, dtype, mp_, h):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "graph-physics_amd")]
+    # 1 MiB buckets: several per step (the decoder alone, groups of processor blocks, the encoders)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MGN_GRAD_BUCKET_MB="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    import __graft_entry__ as ge
+    from graphphysics.utils import meshes
+
+    ge.build()
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    losses, params, bufs, grads = _run({k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}, dtype, mp_, h, True)
+    torch.save({"losses": losses, "params": params, "bufs": bufs, "grads": grads}, os.path.join(out, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype,mp_,h", [(torch.float32, 3, 32), (torch.bfloat16, 4, 128)])
+def test_rccl_overlapped_allreduce_step_equals_single_process(dtype, mp_, h):
+    """The RCCL data-parallel step records the bucketed gradient all-reduce (overlapped with the
+    backward on a communication stream) and AdamW inside the hipGraph (training/step.py,
+    distributed.GradBuckets). On a 1-rank RCCL group every all-reduce is the identity, so the step
+    must equal the single-process captured step exactly: same losses, gradients and parameters
+    bit for bit (a missed or doubled bucket, or a bucket reduced before its gradients were written,
+    shows up here). Run in a child process (one RCCL communicator, torn down with the process)."""
+    import __graft_entry__ as ge
+
+    ge.build()
+    from graphphysics.utils import meshes
+
+    port = 30600 + os.getpid() % 500 + (0 if dtype == torch.float32 else 500)
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_worker_rccl, args=(1, port, out, dtype, mp_, h), nprocs=1, join=True, start_method="spawn")
+        r = torch.load(os.path.join(out, "rccl.pt"), weights_only=True)
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    losses, params, bufs, grads = _run({k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}, dtype, mp_, h, False)
+    assert r["losses"] == losses
+    for a, c in zip(r["grads"], grads):
+        assert torch.equal(a, c)
+    for a, c in zip(r["params"], params):
+        assert torch.equal(a, c)
+    for a, c in zip(r["bufs"], bufs):
+        assert torch.equal(a, c)
