@@ -30,17 +30,6 @@
 #endif
 
 
-// Diagnostics / A-B builds: delay the second and third wave of each SIMD by MGN_STAGGER x 64 cycles
-// (x 1, x 2) after the prologue so the waves sharing a SIMD leave lockstep (0: off)
-#ifndef MGN_STAGGER
-#define MGN_STAGGER 0
-#endif
-__device__ __forceinline__ void stagger(int wave) {
-    if (MGN_STAGGER > 0) {
-        for (int k = 0; k < (wave >> 2); ++k) __builtin_amdgcn_s_sleep(MGN_STAGGER);
-    }
-}
-
 #ifndef MGN_NODE_AG
 #define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
 #endif
@@ -443,7 +432,6 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     for (int i = threadIdx.x; i < 5 * H; i += NWK * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
     __syncthreads();
     if (tile >= a.ntiles) return;
-    stagger(wave);
 #pragma unroll
     for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
     pin(di);
@@ -613,7 +601,6 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
     int ngi = 0;
     if (tile < a.ntiles) {
-        stagger(wave);
         ngi = bidx(a, min(tile + stride, last), lane);
         pin_in<PGA>(nxt);
         pin(ngi);

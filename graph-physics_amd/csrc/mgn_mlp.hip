@@ -1096,9 +1096,14 @@ struct RgArgs {
     RgJob job[12];
 };
 
+// A-B builds only: cache policy of the ring's LDS-DMA streams (bit 0: X operand nt, bit 1: dZ nt)
+#ifndef MGN_RING_NT
+#define MGN_RING_NT 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
 }
 
 __device__ __forceinline__ int rg_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -1128,7 +1133,8 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
         const int64_t m0 = r_begin + (int64_t)sc * RG_RS;
         char* slot = smem + (s % RG_NS) * RG_SLOT;
         // row-major dZ (rows < RP all written, padding rows zero): the X row image's swizzle
-        glds16(zrm ? Z + (m0 + gr) * H + gch * 8 : Z + m0 * H + w * 512 + lane * 8, slot + w * 1024);
+        glds16<(MGN_RING_NT & 2) ? 2 : 0>(zrm ? Z + (m0 + gr) * H + gch * 8 : Z + m0 * H + w * 512 + lane * 8,
+                                          slot + w * 1024);
         const __bf16* xs;
         if (!staged) {
             xs = X + (((m0 >> 3) + (w >> 1)) * job.kp + (w & 1) * 64 + lane) * 8;
@@ -1136,7 +1142,7 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
             const int64_t row = m0 + gr < job.M ? m0 + gr : job.M - 1;
             xs = X + row * job.ld + gch * 8;
         }
-        glds16(xs, slot + RG_SLOT / 2 + w * 1024);
+        glds16<(MGN_RING_NT & 1) ? 2 : 0>(xs, slot + RG_SLOT / 2 + w * 1024);
     };
     f4 acc[2][4];
 #pragma unroll

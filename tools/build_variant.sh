@@ -1,8 +1,16 @@
 #!/bin/bash
-# Diagnostics: relink libmgn with mgn_chain16.hip compiled under extra defines (A/B and ablation
-# studies; never the shipped library). bash tools/build_variant.sh <name> "<defines>"
+# Diagnostics: relink libmgn with ONE source compiled under extra defines (A/B and ablation studies;
+# never the shipped library). bash tools/build_variant.sh <name> "<defines>" [source, default mgn_chain16.hip]
 set -e
 L=graph-physics_amd/graphphysics/_lib
+SRC=${3:-mgn_chain16.hip}
+B=${SRC%.hip}
 mkdir -p $L/var
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable -mllvm -amdgpu-mfma-vgpr-form $2 -I include -c graph-physics_amd/csrc/mgn_chain16.hip -o $L/var/chain16_$1.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $L/mgn_mlp.o $L/var/chain16_$1.o $L/mgn_graph.o $L/mgn_build.o $L/mgn_prof.o -o $L/var/libmgn_$1.so
+EXTRA=""
+[ "$SRC" = "mgn_chain16.hip" ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable $EXTRA $2 -I include -c graph-physics_amd/csrc/$SRC -o $L/var/${B}_$1.o
+OBJS=""
+for s in mgn_mlp mgn_chain16 mgn_graph mgn_build mgn_prof; do
+  if [ $s = $B ]; then OBJS="$OBJS $L/var/${B}_$1.o"; else OBJS="$OBJS $L/$s.o"; fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS -o $L/var/libmgn_$1.so
