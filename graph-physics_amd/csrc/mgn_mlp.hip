@@ -2077,35 +2077,51 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
     T* B = reinterpret_cast<T*>(smem);  // [BM][ldb]: dP_i at column 0, dP_j at column HP
     const int64_t row0 = (int64_t)blockIdx.x * BM;
     const T* dz = reinterpret_cast<const T*>(a.dz0);
-    for (int it = threadIdx.x; it < 2 * BM * CPR; it += MGN_THREADS) {
+    // segment sums, one (direction, row, 16-byte column chunk) item at a time: every item's segment
+    // bounds are loaded up front, then each item gathers its edges in groups of SG with ONE round
+    // trip per group (indices past the segment end re-read its last edge and are not added), in
+    // edge order — the same fp32 sums as an edge-by-edge loop
+    constexpr int NIT = (2 * BM * CPR + MGN_THREADS - 1) / MGN_THREADS, SG = 8;
+    int kbs[NIT], kes[NIT];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+        const int it = threadIdx.x + j * MGN_THREADS;
+        const int s = it / (BM * CPR), r = (it - s * (BM * CPR)) / CPR;
+        const int64_t v = row0 + r;
+        kbs[j] = kes[j] = 0;
+        if (it < 2 * BM * CPR && v < a.N) {
+            const int32_t* ptr = s == 0 ? a.col_ptr : a.row_ptr;
+            kbs[j] = ptr[v];
+            kes[j] = ptr[v + 1];
+        }
+    }
+#pragma unroll 1
+    for (int j = 0; j < NIT; ++j) {
+        const int it = threadIdx.x + j * MGN_THREADS;
+        if (it >= 2 * BM * CPR) break;
         const int s = it / (BM * CPR), rem = it - s * (BM * CPR);
         const int r = rem / CPR, c = (rem - r * CPR) * CH;
-        const int64_t v = row0 + r;
+        const int kb = kbs[j], ke = kes[j];
         float acc[CH];
 #pragma unroll
         for (int e = 0; e < CH; ++e) acc[e] = 0.f;
-        if (v < a.N) {
-            const int32_t* ptr = s == 0 ? a.col_ptr : a.row_ptr;
-            const int kb = ptr[v], ke = ptr[v + 1];
-            int k = kb;
-            for (; k + 4 <= ke; k += 4) {
-                float t[4][CH];
-                int64_t src[4];
+#pragma unroll 1
+        for (int k = kb; k < ke; k += SG) {
+            int64_t src[SG];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) src[u] = s == 0 ? (int64_t)(k + u) : (int64_t)a.row_perm[k + u];
+            for (int u = 0; u < SG; ++u) {
+                const int ku = k + u < ke ? k + u : ke - 1;
+                src[u] = s == 0 ? (int64_t)ku : (int64_t)a.row_perm[ku];
+            }
+            float t[SG][CH];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
+            for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < SG; ++u)
+                if (k + u < ke) {
 #pragma unroll
                     for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
-            }
-            for (; k < ke; ++k) {
-                float t[CH];
-                Chunk<T>::load(dz + (s == 0 ? (int64_t)k : (int64_t)a.row_perm[k]) * H + c, t);
-#pragma unroll
-                for (int e = 0; e < CH; ++e) acc[e] += t[e];
-            }
+                }
         }
         Chunk<T>::store(B + (size_t)r * a.ldb + s * a.HP + c, acc);
     }
