@@ -1,3 +1,5 @@
+#include <vector>
+#include <cstddef>
 // Fused MLP kernels for the MeshGraphNet processor (gfx950).
 //
 // One workgroup (256 threads = 4 waves) owns a tile of BM rows (edges or nodes) and runs the
@@ -1331,18 +1333,19 @@ __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float*
     }
 }
 
-// one launch reducing up to two MLPs (blocks of desc 0, then desc 1)
+// one launch reducing up to RED_MAX MLPs (the blocks of desc 0, then desc 1, ...): a block
+// backward's two MLPs, or every processor block's at the end of the backward (deferred reduction)
+constexpr int RED_MAX = 32;
 struct RedArgs {
-    RedDesc d[2];
+    RedDesc d[RED_MAX];
     int32_t nd, pad;
 };
 __global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(RedArgs a) {
     __shared__ float red[MGN_THREADS];
-    const int64_t b = blockIdx.x;
-    if (a.nd > 1 && b >= a.d[0].blocks)
-        reduce_block(a.d[1], b - a.d[0].blocks, red);
-    else
-        reduce_block(a.d[0], b, red);
+    int64_t b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < a.nd && b >= a.d[i].blocks) b -= a.d[i++].blocks;
+    reduce_block(a.d[i], b, red);
 }
 
 // --------------------------------------------------------------------------- weight packing
@@ -1606,17 +1609,20 @@ RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* 
 }
 
 int launch_reduce2(const RedDesc* d, int nd, hipStream_t st) {
-    RedArgs a;
-    memset(&a, 0, sizeof(a));
-    a.nd = nd;
-    unsigned blocks = 0;
-    for (int i = 0; i < nd; ++i) {
-        a.d[i] = d[i];
-        blocks += (unsigned)d[i].blocks;
+    for (int i0 = 0; i0 < nd; i0 += RED_MAX) {
+        RedArgs a;
+        memset(&a, 0, sizeof(a));
+        a.nd = nd - i0 < RED_MAX ? nd - i0 : RED_MAX;
+        unsigned blocks = 0;
+        for (int i = 0; i < a.nd; ++i) {
+            a.d[i] = d[i0 + i];
+            blocks += (unsigned)a.d[i].blocks;
+        }
+        if (blocks == 0) continue;
+        ProfScope ps(PROF_WGRAD_REDUCE, st);
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, a);
+        MGN_LAUNCH_CHECK();
     }
-    ProfScope ps(PROF_WGRAD_REDUCE, st);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(MGN_THREADS), 0, st, a);
-    MGN_LAUNCH_CHECK();
     return 0;
 }
 
@@ -1806,7 +1812,8 @@ struct BlockWgradIn {
     float *npart, *ngrads;
 };
 
-int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradIn& in, hipStream_t st) {
+int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradIn& in, hipStream_t st,
+                     RedDesc* defer = nullptr) {
     constexpr int H = 128;
     const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
     auto rows_for = [](int64_t RP, int64_t target, int* nch) {
@@ -1898,6 +1905,11 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
                     red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
     (void)re;
+    if (defer) {  // the caller reduces later (mgn_wgrad_reduce_many): slabs + partials must persist
+        defer[0] = d[0];
+        defer[1] = d[1];
+        return 0;
+    }
     return launch_reduce2(d, 2, st);
 }
 
@@ -2462,8 +2474,30 @@ struct BlockBwdCarve {
     bool chained;
 };
 
+// Deferred-reduction "keep" buffer of one block: the RMSNorm-scale partial rows and the weight-
+// gradient slabs of both MLPs, which then outlive the block's call (the caller reduces every block's
+// in one launch, mgn_wgrad_reduce_many). Sizes: the most any launch writes (as mlp_bwd_ws).
+struct KeepLayout {
+    size_t edsp, epart, ndsp, npart, total;
+};
+static KeepLayout keep_layout(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    KeepLayout k;
+    size_t o = 0;
+    const int64_t RPE = rows_pad(t->num_edges), RPN = rows_pad(t->num_nodes);
+    k.edsp = o;
+    o += align_up((size_t)(RPE / 16) * edge->out_dim * sizeof(float));
+    k.epart = o;
+    o += align_up((size_t)wgrad_max_chunks(RPE) * grad_G(edge) * sizeof(float));
+    k.ndsp = o;
+    o += align_up((size_t)(RPN / 16) * node->out_dim * sizeof(float));
+    k.npart = o;
+    o += align_up((size_t)wgrad_max_chunks(RPN) * grad_G(node) * sizeof(float));
+    k.total = o;
+    return k;
+}
+
 static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, void* ws,
-                                     const BlockWs& wl) {
+                                     const BlockWs& wl, void* keep = nullptr) {
     BlockBwdCarve c;
     memset(&c, 0, sizeof(c));
     const int H = edge->hidden, dt = edge->dtype;
@@ -2492,6 +2526,14 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dsp = reinterpret_cast<float*>(p);
     p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
     c.part = reinterpret_cast<float*>(p);
+    if (keep && c.chained) {
+        const KeepLayout k = keep_layout(t, edge, node);
+        char* q = reinterpret_cast<char*>(keep);
+        c.dsp = reinterpret_cast<float*>(q + k.edsp);
+        c.part = reinterpret_cast<float*>(q + k.epart);
+        c.ndsp = reinterpret_cast<float*>(q + k.ndsp);
+        c.npart = reinterpret_cast<float*>(q + k.npart);
+    }
     return c;
 }
 
@@ -2507,17 +2549,15 @@ static int block_bwd_check(const mgn_topology* t, const mgn_mlp* edge, const mgn
     return 0;
 }
 
-int mgn_block_backward_data(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
-                            const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
-                            void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
-                            mgn_stream_t stream) {
-    (void)e;
-    (void)edge_grads;
+static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                                    const mgn_block_saved* saved, const void* dx_out, const void* de_out, void* dx,
+                                    void* de, float* node_grads, void* ws, size_t ws_bytes, void* keep,
+                                    mgn_stream_t stream) {
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
-    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl);
+    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl, keep);
 
     // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
     if (c.chained) {
@@ -2569,18 +2609,25 @@ int mgn_block_backward_data(const mgn_topology* t, const mgn_mlp* edge, const mg
     return rc;
 }
 
-int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
-                             const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
-                             void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
-                             mgn_stream_t stream) {
-    (void)dx_out;
-    (void)dx;
-    (void)de;
+int mgn_block_backward_data(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                            const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                            void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                            mgn_stream_t stream) {
+    (void)e;
+    (void)edge_grads;
+    return block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
+                                    nullptr, stream);
+}
+
+static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                                     const void* e, const mgn_block_saved* saved, const void* de_out,
+                                     float* edge_grads, float* node_grads, void* ws, size_t ws_bytes, void* keep,
+                                     RedDesc* defer, mgn_stream_t stream) {
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
-    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl);
+    const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl, keep);
     const int64_t E = t->num_edges, N = t->num_nodes;
     if (c.chained) {
         BlockWgradIn in;
@@ -2603,7 +2650,7 @@ int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const m
         in.nntiles = chain16_node_backward_parts(N);
         in.npart = c.npart;
         in.ngrads = node_grads;
-        return block_wgrad_ring(edge, node, in, st);
+        return block_wgrad_ring(edge, node, in, st, keep ? defer : nullptr);
     }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
     const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
@@ -2623,6 +2670,66 @@ int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const m
     }
     if (rc) return rc;
     return launch_reduce(edge, c.part, nchunks, c.dsp, ntiles, edge_grads, st);
+}
+
+int mgn_block_backward_wgrad(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                             const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                             void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                             mgn_stream_t stream) {
+    (void)dx_out;
+    (void)dx;
+    (void)de;
+    return block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,
+                                     nullptr, nullptr, stream);
+}
+
+static_assert(sizeof(mgn_wgrad_reduce) == sizeof(RedDesc) && offsetof(mgn_wgrad_reduce, G) == offsetof(RedDesc, G) &&
+                  offsetof(mgn_wgrad_reduce, blocks) == offsetof(RedDesc, blocks),
+              "mgn_wgrad_reduce must mirror RedDesc");
+
+size_t mgn_block_backward_keep_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    return keep_layout(t, edge, node).total;
+}
+
+int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                                const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                                void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                                void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2, mgn_stream_t stream) {
+    MGN_REQUIRE(reduce2, "reduce2 (two mgn_wgrad_reduce) required");
+    memset(reduce2, 0, 2 * sizeof(mgn_wgrad_reduce));
+    BlockWs wl;
+    if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
+    const bool chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
+    if (!chained) {  // generic MLPs: reduced at once, nothing left for the caller
+        if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,
+                                             ws_bytes, nullptr, stream))
+            return r;
+        return block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,
+                                         nullptr, nullptr, stream);
+    }
+    MGN_REQUIRE(keep && keep_bytes >= keep_layout(t, edge, node).total, "block backward keep buffer too small");
+    if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
+                                         keep, stream))
+        return r;
+    RedDesc d[2];
+    memset(d, 0, sizeof(d));
+    if (int r = block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,
+                                          keep, d, stream))
+        return r;
+    memcpy(reduce2, d, sizeof(d));
+    return 0;
+}
+
+int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream) {
+    MGN_REQUIRE(n >= 0 && (n == 0 || reds), "bad reduction list");
+    std::vector<RedDesc> d;
+    for (int32_t i = 0; i < n; ++i) {
+        RedDesc x;
+        memcpy(&x, &reds[i], sizeof(x));
+        if (x.blocks > 0) d.push_back(x);
+    }
+    if (d.empty()) return 0;
+    return launch_reduce2(d.data(), (int)d.size(), (hipStream_t)stream);
 }
 
 int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,

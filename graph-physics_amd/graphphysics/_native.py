@@ -43,6 +43,11 @@ class BlockSaved(ctypes.Structure):
     _fields_ = [("edge", MlpSaved), ("node", MlpSaved), ("aggr", _vp)]
 
 
+class WgradReduce(ctypes.Structure):
+    _fields_ = [("part", _vp), ("dsp", _vp), ("grads", _vp), ("G", _i64), ("nchunks", _i32), ("ntiles", _i32),
+                ("NS", _i32), ("blocks", _i32)]
+
+
 class NormalizerState(ctypes.Structure):
     _fields_ = [("acc_sum", _vp), ("acc_sum_sq", _vp), ("acc_count", _vp), ("num_acc", _vp), ("pending", _vp),
                 ("max_acc", _f32), ("eps", _f32)]
@@ -87,6 +92,11 @@ EXPORTS = {
     "mgn_block_backward_wgrad": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
                                         _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _sz, _vp]),
+    "mgn_block_backward_keep_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp)]),
+    "mgn_block_backward_deferred": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                           _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _vp]),
+    "mgn_wgrad_reduce_many": (_i32, [ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),

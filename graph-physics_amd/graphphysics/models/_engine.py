@@ -78,6 +78,9 @@ def _grad_ready(G, lo, hi):
 # processor blocks hand the next block's node projections over from their node-MLP kernel
 # (mgn_block_forward_chain); False: every block launches its own projection kernel (tests compare)
 CHAIN_PROJ = True
+# processor blocks' weight-gradient reductions deferred to one launch after the last block
+# (mgn_block_backward_deferred + mgn_wgrad_reduce_many); False: one reduction per block (same sums)
+DEFER_REDUCE = True
 _SIDE = {}
 
 
@@ -443,6 +446,16 @@ class EPDFunction(torch.autograd.Function):
         # stream, overlapped with the next block's data half (two workspaces alternate; a workspace is
         # reused only after the side stream has finished with it). Joined before returning.
         overlap = OVERLAP_WGRAD and nb > 1
+        # deferred weight-gradient reductions: each block leaves its slabs in its own keep buffer and
+        # ONE launch reduces them all after the last block (not when a gradient-ready callback needs
+        # each block's gradients as soon as its backward ends)
+        defer = DEFER_REDUCE and not overlap and GRAD_READY is None and nb > 0
+        if defer:
+            kb = max(int(L.mgn_block_backward_keep_bytes(ctypes.byref(topo.struct), ctypes.byref(bdescs[0]),
+                                                         ctypes.byref(bdescs[1]))), 256)
+            kb = (kb + 255) // 256 * 256
+            keep = torch.empty(nb * kb, dtype=torch.uint8, device=dev)
+            reds = (nat.WgradReduce * (2 * nb))()
         if overlap:
             main = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
@@ -455,7 +468,12 @@ class EPDFunction(torch.autograd.Function):
                     nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
                     nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
                     ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
-            if not overlap:
+            if defer:
+                nat.check(L.mgn_block_backward_deferred(*args, nat.ptr(ws), ws.numel(),
+                                                        ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
+                                                        ctypes.pointer(reds[2 * b]),
+                                                        st))
+            elif not overlap:
                 nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
                 _grad_ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
             else:
@@ -471,6 +489,8 @@ class EPDFunction(torch.autograd.Function):
                 ev.record(side)
                 done[b % 2] = ev
             dx, de = dx1, de1
+        if defer:
+            nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
         if overlap:
             for ev in done:
                 if ev is not None:

@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 8
+#define MGN_ABI_VERSION 9
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -195,6 +195,28 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
                        const void* dx_out, const void* de_out, void* dx, void* de,
                        float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                        mgn_stream_t stream);
+/* Deferred weight-gradient reduction (a processor stack's backward, processors.py:129-131 in
+ * reverse): mgn_block_backward_deferred is mgn_block_backward except that, for the chained bf16
+ * h=128 MLPs, the fixed-order reduction of the weight-gradient slabs is NOT launched: the slabs and
+ * RMSNorm-scale partials go to `keep` (mgn_block_backward_keep_bytes, one buffer per block, alive
+ * until the reduction) and reduce2[0..1] describe the reduction; mgn_wgrad_reduce_many then runs
+ * every block's in ONE launch — the same sums in the same order, one launch instead of one per
+ * block. Generic MLPs are reduced at once (reduce2 zeroed: nothing to do). */
+typedef struct mgn_wgrad_reduce {
+    const float* part;
+    const float* dsp;
+    float* grads;
+    int64_t G;
+    int32_t nchunks, ntiles, NS, blocks;
+} mgn_wgrad_reduce;
+size_t mgn_block_backward_keep_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node);
+int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                                const void* x, const void* e, const mgn_block_saved* saved,
+                                const void* dx_out, const void* de_out, void* dx, void* de,
+                                float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                                void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
+                                mgn_stream_t stream);
+int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream);
 /* The same backward as two calls over one workspace (same arguments): _data writes dx, de (and, for
  * MLPs outside the chained bf16 h=128 kernels, the node-MLP weight gradients); _wgrad then writes the
  * weight gradients from what _data left in `ws` plus the forward saves, and may run on another

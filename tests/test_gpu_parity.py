@@ -812,3 +812,31 @@ def test_chained_projection_handoff_matches_per_block_projections(train):
     assert rel(outs[0][0], outs[1][0]) <= 1e-2, rel(outs[0][0], outs[1][0])
     for a, c in zip(outs[0][1], outs[1][1]):
         assert rel(a, c) <= 1e-2, rel(a, c)
+
+
+def test_deferred_weight_gradient_reduction_is_bitwise_identical():
+    """mgn_block_backward_deferred + mgn_wgrad_reduce_many (every processor block's slab reduction in
+    ONE launch after the last block) sums the same slabs in the same fixed order as the per-block
+    reduction: the gradients are bit-identical."""
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(2, jitter=0.01)
+    g = Data(x=torch.randn(b["x"].shape[0], 11, device=DEV), edge_index=torch.from_numpy(b["edge_index"]).to(DEV),
+             edge_attr=torch.from_numpy(b["edge_attr"]).to(DEV))
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(4, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
+    grads = []
+    for defer in (True, False):
+        _engine.DEFER_REDUCE = defer
+        try:
+            y = m(g)
+            y.backward(torch.ones_like(y))
+            grads.append([p.grad.clone() for p in m.parameters()])
+            m.zero_grad(set_to_none=True)
+        finally:
+            _engine.DEFER_REDUCE = True
+    for a, c in zip(*grads):
+        assert torch.equal(a, c)
