@@ -1295,12 +1295,51 @@ struct RedDesc {
     int32_t nchunks, ntiles, NS, blocks;
 };
 
+// 16-byte form of the slab sum: a thread sums 4 consecutive outputs (the same per-output order as
+// the scalar form: chunk group cg = c mod 4, chunks in increasing order, groups combined 0+1+2+3)
+__device__ __forceinline__ bool red_vec(const RedDesc& d) {
+    return (d.G & 3) == 0 && ((uintptr_t)d.part & 15) == 0;
+}
+__device__ __forceinline__ int64_t red_gblocks(const RedDesc& d) {
+    return red_vec(d) ? (d.G + 255) / 256 : (d.G + 63) / 64;
+}
+
 __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float* red) {
-    const int64_t gblocks = (d.G + 63) / 64;
+    const int64_t gblocks = red_gblocks(d);
     const int tid = threadIdx.x;
     const float* part = d.part;
     const int64_t G = d.G;
-    if (b < gblocks) {
+    if (b < gblocks && red_vec(d)) {
+        const int64_t g = b * 256 + 4 * (tid & 63);
+        const int cg = tid >> 6;
+        f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+        if (g < G) {
+            int c = cg;
+            for (; c + 12 < d.nchunks; c += 16) {
+                const f4 v0 = *reinterpret_cast<const f4*>(part + (int64_t)c * G + g);
+                const f4 v1 = *reinterpret_cast<const f4*>(part + (int64_t)(c + 4) * G + g);
+                const f4 v2 = *reinterpret_cast<const f4*>(part + (int64_t)(c + 8) * G + g);
+                const f4 v3 = *reinterpret_cast<const f4*>(part + (int64_t)(c + 12) * G + g);
+                sum += v0;
+                sum += v1;
+                sum += v2;
+                sum += v3;
+            }
+            for (; c < d.nchunks; c += 4) sum += *reinterpret_cast<const f4*>(part + (int64_t)c * G + g);
+        }
+        f4* r4 = reinterpret_cast<f4*>(red);
+        r4[tid] = sum;
+        __syncthreads();
+        if (tid < 64 && g < G) {
+            const f4 v = ((r4[tid] + r4[tid + 64]) + r4[tid + 128]) + r4[tid + 192];
+            if (((uintptr_t)(d.grads + g) & 15) == 0) {
+                *reinterpret_cast<f4*>(d.grads + g) = v;
+            } else {  // the flat gradient buffer puts a block's slice at any 4-byte offset
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d.grads[g + q] = v[q];
+            }
+        }
+    } else if (b < gblocks) {
         const int64_t g = b * 64 + (tid & 63);
         const int cg = tid >> 6;
         float s = 0.f;
@@ -1341,7 +1380,7 @@ struct RedArgs {
     int32_t nd, pad;
 };
 __global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(RedArgs a) {
-    __shared__ float red[MGN_THREADS];
+    __shared__ __attribute__((aligned(16))) float red[4 * MGN_THREADS];
     int64_t b = blockIdx.x;
     int i = 0;
     while (i + 1 < a.nd && b >= a.d[i].blocks) b -= a.d[i++].blocks;
@@ -1604,7 +1643,8 @@ RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* 
     d.nchunks = nchunks;
     d.ntiles = ntiles;
     d.NS = m->has_norm ? m->out_dim : 0;
-    d.blocks = (int32_t)(cdiv64(d.G, 64) + d.NS);
+    const bool vec = (d.G & 3) == 0 && ((uintptr_t)part & 15) == 0;
+    d.blocks = (int32_t)(cdiv64(d.G, vec ? 256 : 64) + d.NS);  // = red_gblocks + NS
     return d;
 }
 
