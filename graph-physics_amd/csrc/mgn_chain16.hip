@@ -600,6 +600,8 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     // over the tile's 16 edges, then the 4 lane-group leaders add their features; fixed order)
     for (int i = lane; i < H; i += 64) red[wave * H + i] = 0.f;
     int ngi = 0;
+    u32x2 gac[8];       // !PGA: d_aggr[dst] of the current tile
+    bool gpre = false;  // gac already loaded (by the previous iteration)
     if (tile < a.ntiles) {
         ngi = bidx(a, min(tile + stride, last), lane);
         pin_in<PGA>(nxt);
@@ -612,8 +614,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         // RMSNorm backward (layers.py:59-74) from the prefetched tile
         f4 acc[8];
         float dot = 0.f;
-        u32x2 gac[8];
-        if constexpr (!PGA) {
+        if (!PGA && !gpre) {  // first tile: its gather now; later tiles': issued under the de stores
             const __bf16* gp = a.gath + (int64_t)gcur * H + 4 * g;
 #pragma unroll
             for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
@@ -682,6 +683,12 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 8; ++t)
             if (!ZD) acc[t] += bf4(dre[t]);
+        if constexpr (!PGA) {  // the next tile's gather, under this tile's de stores
+            const __bf16* gp = a.gath + (int64_t)ngi * H + 4 * g;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+            gpre = true;
+        }
         store_rows(acc, scr, a.de, tile, a.M, lane);
         STAMP(7);
         pin_in<PGA>(nxt);
