@@ -21,7 +21,7 @@
 
 // Diagnostics builds only (-DMGN_ABLATE=bits, results wrong when nonzero; see mgn_mlp.hip): edge
 // forward 1 = P gathers from row 0 (cache-resident), 2 = no P loads, 4 = no weight-staging loads,
-// 8 = no stores of outputs / saves
+// 8 = no stores of outputs / saves; node forward 16 = no aggregation gathers
 #ifndef MGN_ABLATE
 #define MGN_ABLATE 0
 #endif
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
 #pragma unroll
         for (int t = 0; t < 8; ++t) agg[t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-        for (int k = kb; k < ke; k += AG) {
+        for (int k = kb; k < ((MGN_ABLATE & 16) ? kb : ke); k += AG) {  // ablation 16: no aggregation
             u32x2 zz[AG][8];
             float rr[AG];
 #pragma unroll

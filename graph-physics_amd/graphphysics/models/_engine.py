@@ -15,6 +15,7 @@ Device memory is always allocated here through the PyTorch caching allocator; th
 none. No CPU fallback exists: tensors must live on a HIP device.
 """
 import ctypes
+import os
 import weakref
 
 import torch
@@ -61,7 +62,7 @@ class GraphTopology:
 
 # the block backward's weight-gradient halves run on a side stream, overlapped with the next block's
 # data half (set False to serialise them on the current stream, e.g. for A/B timing; same results)
-OVERLAP_WGRAD = False
+OVERLAP_WGRAD = os.environ.get("MGN_OVERLAP_WGRAD", "0") == "1"
 # Gradient-ready callback (data parallelism): EncodeProcessDecode's backward calls
 # GRAD_READY(G, lo, hi) on the current stream as soon as the flat-gradient range [lo, hi) is final —
 # the decoder's, then each processor block's (last block first), then the encoders' — so a
