@@ -1293,7 +1293,15 @@ struct RedDesc {
     float* grads;
     int64_t G;
     int32_t nchunks, ntiles, NS, blocks;
+    // optional column region of W0 ([w0_n][w0_k] at the start of the slab rows): columns >= xcol0
+    // sum only their first nchunks_x slabs (w0_k == 0: none)
+    int32_t w0_n, w0_k, xcol0, nchunks_x;
 };
+// slabs summed for output g
+__device__ __forceinline__ int red_nchunks(const RedDesc& d, int64_t g) {
+    if (d.w0_k > 0 && g < (int64_t)d.w0_n * d.w0_k && (int)(g % d.w0_k) >= d.xcol0) return d.nchunks_x;
+    return d.nchunks;
+}
 
 // 16-byte form of the slab sum: a thread sums 4 consecutive outputs (the same per-output order as
 // the scalar form: chunk group cg = c mod 4, chunks in increasing order, groups combined 0+1+2+3)
@@ -1313,9 +1321,10 @@ __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float*
         const int64_t g = b * 256 + 4 * (tid & 63);
         const int cg = tid >> 6;
         f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+        const int nch = g < G ? red_nchunks(d, g) : 0;  // one column region per 4 outputs (k0 % 4 == 0)
         if (g < G) {
             int c = cg;
-            for (; c + 12 < d.nchunks; c += 16) {
+            for (; c + 12 < nch; c += 16) {
                 const f4 v0 = *reinterpret_cast<const f4*>(part + (int64_t)c * G + g);
                 const f4 v1 = *reinterpret_cast<const f4*>(part + (int64_t)(c + 4) * G + g);
                 const f4 v2 = *reinterpret_cast<const f4*>(part + (int64_t)(c + 8) * G + g);
@@ -1325,7 +1334,7 @@ __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float*
                 sum += v2;
                 sum += v3;
             }
-            for (; c < d.nchunks; c += 4) sum += *reinterpret_cast<const f4*>(part + (int64_t)c * G + g);
+            for (; c < nch; c += 4) sum += *reinterpret_cast<const f4*>(part + (int64_t)c * G + g);
         }
         f4* r4 = reinterpret_cast<f4*>(red);
         r4[tid] = sum;
@@ -1344,8 +1353,9 @@ __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float*
         const int cg = tid >> 6;
         float s = 0.f;
         if (g < G) {
+            const int nch = red_nchunks(d, g);
             int c = cg;
-            for (; c + 12 < d.nchunks; c += 16) {
+            for (; c + 12 < nch; c += 16) {
                 const float v0 = part[(int64_t)c * G + g], v1 = part[(int64_t)(c + 4) * G + g];
                 const float v2 = part[(int64_t)(c + 8) * G + g], v3 = part[(int64_t)(c + 12) * G + g];
                 s += v0;
@@ -1353,7 +1363,7 @@ __device__ __forceinline__ void reduce_block(const RedDesc& d, int64_t b, float*
                 s += v2;
                 s += v3;
             }
-            for (; c < d.nchunks; c += 4) s += part[(int64_t)c * G + g];
+            for (; c < nch; c += 4) s += part[(int64_t)c * G + g];
         }
         red[tid] = s;
         __syncthreads();
@@ -1643,6 +1653,8 @@ RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* 
     d.nchunks = nchunks;
     d.ntiles = ntiles;
     d.NS = m->has_norm ? m->out_dim : 0;
+    d.w0_n = d.w0_k = d.xcol0 = 0;
+    d.nchunks_x = nchunks;
     const bool vec = (d.G & 3) == 0 && ((uintptr_t)part & 15) == 0;
     d.blocks = (int32_t)(cdiv64(d.G, vec ? 256 : 64) + d.NS);  // = red_gblocks + NS
     return d;
@@ -1865,20 +1877,23 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
         *nch = (int)cdiv64(RP, r);
         return (int)r;
     };
-    // one round of workgroups: 4 edge + 2 projection jobs on ce chunks, 5 node jobs on cn chunks with
-    // cn/ce ≈ RPN/RPE (equal rows per workgroup), 6·ce + 5·cn <= CUs
+    // one round of workgroups, every one over about the same number of rows: 4 edge jobs on ce
+    // chunks, 5 node jobs on cn chunks, the 2 W0-projection jobs (node rows, into the edge slabs'
+    // x-block columns) on cp = cn chunks — the reduction sums only the first cp slabs of those
+    // columns (RedDesc x-columns), so the projections need not be cut into ce short chunks
     const int cus = device_cus();
-    int64_t ce0 = (int64_t)((double)cus / (6.0 + 5.0 * (double)RPN / (double)RPE));
-    if (ce0 < 1) ce0 = 1;
-    int ce, cn, cp;
+    int ce = 1, cn = 1, cp = 1;
     int re = 0, rn = 0;
-    for (;; --ce0) {
-        re = rows_for(RPE, cdiv64(RPE, ce0), &ce);
-        rn = rows_for(RPN, re, &cn);
-        if (6 * ce + 5 * cn <= cus || ce0 == 1) break;
+    {
+        const int64_t total = 4 * RPE + 7 * RPN;
+        for (int64_t target = cdiv64(cdiv64(total, cus), 64) * 64;; target += 64) {
+            re = rows_for(RPE, target, &ce);
+            rn = rows_for(RPN, target, &cn);
+            if (4 * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
+        }
+        cp = cn;
     }
-    const int rp = (int)(cdiv64(cdiv64(RPN, ce), 64) * 64);  // the projections fill the edge slabs
-    (void)cp;
+    const int rp = rn;
     RgArgs r;
     memset(&r, 0, sizeof(r));
     int nj = 0, wg = 0;
@@ -1939,11 +1954,16 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     // x blocks of the edge W0 over node rows, into the edge slabs (chunks past N write zeros)
     for (int s2 = 0; s2 < 2; ++s2)
         add(dP + (int64_t)s2 * RPN * H, in.x, H, RPN, in.N, in.epart, Ge, 0, -1, H, edge->in_dim, edge->in_dim,
-            (1 + s2) * H, rp, ce);
+            (1 + s2) * H, rp, cp);
     r.njobs = nj;
     if (int e2 = launch_ring(r, st, PROF_WGRAD)) return e2;
     RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
                     red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
+    // W0 [H][3H] of the edge MLP: its x-block columns [H, 3H) hold cp slabs (the projection jobs)
+    d[0].w0_n = H;
+    d[0].w0_k = edge->in_dim;
+    d[0].xcol0 = H;
+    d[0].nchunks_x = cp;
     (void)re;
     if (defer) {  // the caller reduces later (mgn_wgrad_reduce_many): slabs + partials must persist
         defer[0] = d[0];

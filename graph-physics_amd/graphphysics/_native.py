@@ -45,7 +45,7 @@ class BlockSaved(ctypes.Structure):
 
 class WgradReduce(ctypes.Structure):
     _fields_ = [("part", _vp), ("dsp", _vp), ("grads", _vp), ("G", _i64), ("nchunks", _i32), ("ntiles", _i32),
-                ("NS", _i32), ("blocks", _i32)]
+                ("NS", _i32), ("blocks", _i32), ("w0_n", _i32), ("w0_k", _i32), ("xcol0", _i32), ("nchunks_x", _i32)]
 
 
 class NormalizerState(ctypes.Structure):

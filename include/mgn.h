@@ -208,6 +208,7 @@ typedef struct mgn_wgrad_reduce {
     float* grads;
     int64_t G;
     int32_t nchunks, ntiles, NS, blocks;
+    int32_t w0_n, w0_k, xcol0, nchunks_x; /* W0 columns >= xcol0 sum only nchunks_x slabs */
 } mgn_wgrad_reduce;
 size_t mgn_block_backward_keep_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node);
 int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
