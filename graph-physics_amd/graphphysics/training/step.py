@@ -143,6 +143,25 @@ class TrainStep:
         if on_record is not None:
             on_record()
         self._prologue()  # pending statistics exist before recording (the graph reads their buffers)
+        try:
+            g, loss = self._record()
+        except Exception as ex:  # noqa: BLE001 — an RCCL stack that cannot record collectives
+            if not self.overlap:
+                raise
+            import warnings
+
+            warnings.warn("recording the overlapped gradient all-reduce failed (%s); the all-reduce runs "
+                          "after the replay instead" % ex)
+            self.overlap = False
+            self.opt.zero_grad(set_to_none=True)
+            self._prologue()
+            g, loss = self._record()
+        self.graph, self.static_loss = g, loss
+        self._graph_grads = [p.grad for p in self.params]
+        self._gflat = flat_grad_buffer(self.params)
+        return self
+
+    def _record(self):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._loss()
@@ -167,10 +186,7 @@ class TrainStep:
                 loss.backward(self._seed(loss))
                 if not self.dp:
                     self.opt.launch()
-        self.graph, self.static_loss = g, loss
-        self._graph_grads = [p.grad for p in self.params]
-        self._gflat = flat_grad_buffer(self.params)
-        return self
+        return g, loss
 
     def _bind_graph_grads(self):
         """p.grad -> the captured step's gradient buffer (eager() / zero_grad() may have moved it)."""
