@@ -109,7 +109,11 @@ class Rollout:
         self._topo = _engine.get_topology(self._sei, self._sx.size(0))
         self._sx.copy_(batch.x)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        import torch.distributed as dist
+
+        # a process group's watchdog thread queries events while this thread records (see TrainStep)
+        mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             pred, prev = self._predict(fr, self._last, self._lastp)
             self._last.copy_(pred)
             if self.use_prev:

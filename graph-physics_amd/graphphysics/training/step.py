@@ -163,7 +163,10 @@ class TrainStep:
 
     def _record(self):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # with a process group, the RCCL watchdog thread queries its events while this thread records:
+        # "global" capture mode would turn that query into hipErrorStreamCaptureUnsupported (abort)
+        mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             loss = self._loss()
             if self.overlap:
                 from graphphysics.models import _engine
