@@ -121,15 +121,16 @@ def class_work(n, e, h, mp, lay, nparams, nweights, es):
     the class processes; the reference algorithm's FLOPs, so the split-layer-0 reformulation is not
     credited with work it skips): ("mfma", FLOPs) or ("hbm", bytes).
       edge MLP 12h²/edge fwd (a2): fwd_edge does the e block of layer 0 + the 3 hidden Linears (8h²),
-      proj the x_i / x_j blocks of layer 0 (4h²/edge, applied per node); backward data the same split
+      the x_i / x_j blocks of layer 0 (4h²/edge, applied per node) run in proj for block 0 and inside
+      the previous block's node-MLP forward for blocks 1.. (ABI v8 hand-off); backward data the same split
       (bwd_edge 8h², combine 4h²); weight gradients 12h²/edge + 10h²/node in one ring launch; node MLP
       10h²/node (a3); encoders/decoder 2(in·h + 3h²) per row and 2(3h² + h·out) (a7).
       AdamW: p, g, m, v read + p, m, v written (28 B/param); pack: fp32 weights in, 2 bf16 copies out."""
     enc = 2 * (lay["edge_in"] * h + 3 * h * h) * e + 2 * (lay["node_in"] * h + 3 * h * h) * n
     dec = 2 * (3 * h * h + h * lay["out"]) * n
     return {
-        "fwd_edge": ("mfma", mp * 8 * h * h * e), "proj": ("mfma", mp * 4 * h * h * e),
-        "fwd_node": ("mfma", mp * 10 * h * h * n), "bwd_edge": ("mfma", mp * 8 * h * h * e),
+        "fwd_edge": ("mfma", mp * 8 * h * h * e), "proj": ("mfma", min(mp, 1) * 4 * h * h * e),
+        "fwd_node": ("mfma", mp * 10 * h * h * n + max(mp - 1, 0) * 4 * h * h * e), "bwd_edge": ("mfma", mp * 8 * h * h * e),
         "combine": ("mfma", mp * 4 * h * h * e), "bwd_node": ("mfma", mp * 10 * h * h * n),
         "wgrad": ("mfma", mp * (12 * h * h * e + 10 * h * h * n)),
         "fwd_dense": ("mfma", enc + dec), "bwd_dense": ("mfma", enc + dec), "wgrad_dense": ("mfma", enc + dec),
