@@ -105,11 +105,13 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
                           float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
 // edge MLP forward / backward: 16x16x32 tiles, 12 waves per workgroup (three per SIMD);
 // nparts: number of dscale partial rows written (the reduction's row count)
+// Pair layout (mgn_chain16.hip col_of): the bf16 node projections P are always in it; z_p2 / p2 =
+// the block's node MLP is chained too (then the edge z and d_aggr rows are in it as well)
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st);
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2);
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st);
+                          hipStream_t st, bool p2);
 // dense MLP in_dim <= 32 -> 128 -> 128 -> 128 -> 128 + RMSNorm, bf16 (the encoders): 16-row chained
 // kernels with the generic DENSE save layout (ReLU masks: chained lane words)
 bool chain_dense_eligible(const mgn_mlp* m);

@@ -284,13 +284,32 @@ __device__ __forceinline__ void to_operand(const f4 (&v)[8], bf16x8 (&B)[4]) {
         for (int j = 0; j < 8; ++j) B[s][j] = (__bf16)v[2 * s + (j >> 2)][j & 3];
 }
 
-// write this lane's 32 values of row m (&7) of one octet into the scratch
+// Pair layout (P2) of a bf16 row of 128 features, for rows this library both writes and gathers
+// back in the accumulator layout (node projections P, the edge MLP's z, the node MLP's z, d_aggr):
+// feature 16t + 4g + r sits at 32(t>>1) + 8g + 4(t&1) + r, so the two quads of lane group g for the
+// tile pair (2i, 2i+1) are one 16-byte load (4 loads of 16 B per row and lane instead of 8 of 8 B).
+template <bool P2>
+__device__ __forceinline__ int col_of(int t, int g) {
+    return P2 ? 32 * (t >> 1) + 8 * g + 4 * (t & 1) : 16 * t + 4 * g;
+}
+// the 8 accumulator-layout quads (features 16t + 4g .. +3) of a P2 row
+__device__ __forceinline__ void load_p2(u32x2 (&o)[8], const __bf16* row, int g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(row + 32 * i + 8 * g);
+        o[2 * i] = u32x2{w[0], w[1]};
+        o[2 * i + 1] = u32x2{w[2], w[3]};
+    }
+}
+
+// write this lane's 32 values of row m (&7) of one octet into the scratch (P2: pair layout)
+template <bool P2 = false>
 __device__ __forceinline__ void scr_write(const f4 (&v)[8], __bf16* scr, int lane) {
     const int m = lane & 15, g = lane >> 4;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         const bf16x4 w = {(__bf16)v[t][0], (__bf16)v[t][1], (__bf16)v[t][2], (__bf16)v[t][3]};
-        *reinterpret_cast<bf16x4*>(scr + (m & 7) * SLD + 16 * t + 4 * g) = w;
+        *reinterpret_cast<bf16x4*>(scr + (m & 7) * SLD + col_of<P2>(t, g)) = w;
     }
 }
 
@@ -321,7 +340,9 @@ __device__ __forceinline__ void store_r8(const f4 (&v)[8], __bf16* scr, __bf16* 
     }
 }
 
-// The wave's tile as bf16 rows of a row-major [M][128] matrix (rows >= M skipped), 16-byte stores.
+// The wave's tile as bf16 rows of a row-major [M][128] matrix (rows >= M skipped), 16-byte stores
+// (P2: each row in the pair layout).
+template <bool P2 = false>
 __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16* dst, int64_t tile, int64_t M,
                                            int lane, int64_t ld = H) {
     const int m = lane & 15;
@@ -331,18 +352,18 @@ __device__ __forceinline__ void store_rows(const f4 (&v)[8], __bf16* scr, __bf16
     (void)scr;
     const int64_t row = tile * TR + m;
     if (row < M && !(MGN_ABLATE & 8)) {
-        __bf16* p = dst + row * ld + 4 * (lane >> 4);
+        __bf16* p = dst + row * ld;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const bf16x4 w = {(__bf16)v[t][0], (__bf16)v[t][1], (__bf16)v[t][2], (__bf16)v[t][3]};
-            *reinterpret_cast<bf16x4*>(p + 16 * t) = w;
+            *reinterpret_cast<bf16x4*>(p + col_of<P2>(t, lane >> 4)) = w;
         }
     }
     return;
 #endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        if ((m >> 3) == u) scr_write(v, scr, lane);
+        if ((m >> 3) == u) scr_write<P2>(v, scr, lane);
         lds_fence();
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -411,8 +432,10 @@ __device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, in
 }
 
 // SAVE = false: inference (no autograd): only z and rden (the node MLP's aggregation inputs) are
-// written — no R8 layer inputs, no ReLU masks (≈ 40 % of the training forward's HBM bytes)
-template <bool SAVE, int NWK>
+// written — no R8 layer inputs, no ReLU masks (≈ 40 % of the training forward's HBM bytes).
+// P is in the pair layout; ZP2: z too (the chained node MLP and the chained backward read it so;
+// false: row-major, for a generic node MLP)
+template <bool SAVE, int NWK, bool ZP2>
 __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -445,13 +468,8 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) pi[t] = pj[t] = u32x2{0u, 0u};
         } else {
-            const __bf16* p0 = a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : di) * (2 * H) + 4 * g;
-            const __bf16* p1 = a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : dj) * (2 * H) + H + 4 * g;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                pi[t] = *reinterpret_cast<const u32x2*>(p0 + 16 * t);
-                pj[t] = *reinterpret_cast<const u32x2*>(p1 + 16 * t);
-            }
+            load_p2(pi, a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : di) * (2 * H), g);
+            load_p2(pj, a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : dj) * (2 * H) + H, g);
         }
         int ndi, ndj;
         load_idx(a, min(tile + stride, last), lane, ndi, ndj);
@@ -506,7 +524,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         const float q = sqrtf(ss) * a.dinv + RMS_EPS;
         const float rq = __builtin_amdgcn_rcpf(q);  // bf16 outputs: z·(1/q) is within 2 fp32 ulp of z/q
         if (g == 0 && row < a.M) a.rden_save[row] = q;
-        store_rows(acc, scr, a.z_save, tile, a.M, lane);
+        store_rows<ZP2>(acc, scr, a.z_save, tile, a.M, lane);
         STAMP(5);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -539,7 +557,8 @@ struct BIn16 {  // raw bf16: features 16t + 4g .. +3
 
 // ZD: de_out is identically zero (the processor's last block: EncodeProcessDecode returns nodes only)
 // PGA: prefetch the d_aggr gather with the rest (false: the tile loads it itself, 16 VGPRs fewer)
-template <bool ZD, bool PGA = true>
+// P2: z and the d_aggr rows in the pair layout (written by the chained node MLP kernels)
+template <bool ZD, bool P2, bool PGA = true>
 __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
     const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
     const int off = 4 * (lane >> 4);
@@ -549,8 +568,12 @@ __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t 
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         in.d[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
-        if (PGA) in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
-        in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
+        if (PGA && !P2) in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+        if (!P2) in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
+    }
+    if (P2) {
+        if (PGA) load_p2(in.ga, a.gath + (int64_t)gi * H, lane >> 4);
+        load_p2(in.z, a.z_save + row * H, lane >> 4);
     }
     in.q = a.rden_save[row];
 #pragma unroll
@@ -574,7 +597,7 @@ __device__ __forceinline__ void pin_in(const S& in) {
     for (int l = 0; l < 3; ++l) pin(in.mask[l]);
 }
 
-template <bool ZD, int NWK>
+template <bool ZD, int NWK, bool P2>
 __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -593,7 +616,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     int gcur = gi0;
     stage16<4, NWK * 64>(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
-    bload<ZD, PGA>(nxt, a, min(tile, last), gi0, lane);
+    bload<ZD, P2, PGA>(nxt, a, min(tile, last), gi0, lane);
     for (int i = threadIdx.x; i < H; i += NWK * 64) vec[i] = a.scale[i];
     __syncthreads();
     // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
@@ -615,9 +638,13 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         f4 acc[8];
         float dot = 0.f;
         if (!PGA && !gpre) {  // first tile: its gather now; later tiles': issued under the de stores
-            const __bf16* gp = a.gath + (int64_t)gcur * H + 4 * g;
+            if (P2) {
+                load_p2(gac, a.gath + (int64_t)gcur * H, g);
+            } else {
+                const __bf16* gp = a.gath + (int64_t)gcur * H + 4 * g;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+                for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+            }
         }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -655,7 +682,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
         for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
         STAMP(1);
-        bload<ZD, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
+        bload<ZD, P2, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
         bf16x8 B[4];
         to_operand(acc, B);
@@ -684,9 +711,13 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         for (int t = 0; t < 8; ++t)
             if (!ZD) acc[t] += bf4(dre[t]);
         if constexpr (!PGA) {  // the next tile's gather, under this tile's de stores
-            const __bf16* gp = a.gath + (int64_t)ngi * H + 4 * g;
+            if (P2) {
+                load_p2(gac, a.gath + (int64_t)ngi * H, g);
+            } else {
+                const __bf16* gp = a.gath + (int64_t)ngi * H + 4 * g;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+                for (int t = 0; t < 8; ++t) gac[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
+            }
             gpre = true;
         }
         store_rows(acc, scr, a.de, tile, a.M, lane);
@@ -811,9 +842,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
 #pragma unroll
             for (int u = 0; u < AG; ++u) {
                 const int ku = k + u < ke ? k + u : ke - 1;
-                const __bf16* zp = a.agg_z + (int64_t)ku * H + 4 * g;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) zz[u][t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
+                load_p2(zz[u], a.agg_z + (int64_t)ku * H, g);  // the edge forward's z: pair layout
                 rr[u] = a.agg_rden[ku];
             }
 #pragma unroll
@@ -906,7 +935,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         const float rq = __builtin_amdgcn_rcpf(q);
         if (SAVE) {
             if (g == 0 && ok) a.rden_save[row] = q;
-            store_rows(acc, scr, a.z_save, tile, a.M, lane);
+            store_rows<true>(acc, scr, a.z_save, tile, a.M, lane);  // read back by the node backward only
         }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -936,7 +965,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                         pacc[t] += f4{b[0], b[1], b[2], b[3]};
                     }
                 }
-                store_rows(pacc, scr, a.pn_out + half * H, tile, a.M, lane, 2 * H);
+                store_rows<true>(pacc, scr, a.pn_out + half * H, tile, a.M, lane, 2 * H);
             }
         }
         STAMP(3);
@@ -965,12 +994,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         const int64_t v = clamp_row(row, a.M);
         u32x2 zr[8];
         const __bf16* dp = a.dout + v * H + 4 * g;
-        const __bf16* zp = a.z_save + v * H + 4 * g;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
-            zr[t] = *reinterpret_cast<const u32x2*>(zp + 16 * t);
-        }
+        for (int t = 0; t < 8; ++t) d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
+        load_p2(zr, a.z_save + v * H, g);  // the node forward's z: pair layout
         const float qd = a.rden_save[v];
 #pragma unroll
         for (int l = 0; l < 3; ++l) mk[l] = ok ? a.mask32[l * a.mask_stride * 2 + tl * 64 + lane] : 0u;
@@ -1058,7 +1084,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
                 for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], B[s], acc[t]);
             }
         }
-        store_rows(acc, scr, a.d_aggr, tile, a.M, lane);
+        store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // gathered by the chained edge backward
         STAMP(2);
     }
     STAMP_PRINT("nbwd16");
@@ -1409,7 +1435,7 @@ int set_lds_once(const void* fn, size_t bytes) {
 }  // namespace
 
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st) {
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2) {
     ChainFwdArgs a;
     memset(&a, 0, sizeof(a));
     a.e = reinterpret_cast<const __bf16*>(e);
@@ -1432,8 +1458,14 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
     a.mask_stride = mask_words_per_layer(*m, M);
     if (a.ntiles == 0) return 0;
     const int nwk = edge_waves();
-    const auto kern = nwk == 12 ? (sv->act ? chain16_fwd_kernel<true, 12> : chain16_fwd_kernel<false, 12>)
-                                : (sv->act ? chain16_fwd_kernel<true, 8> : chain16_fwd_kernel<false, 8>);
+    // inference (no saves) always feeds the chained node MLP: z in the pair layout
+    MGN_REQUIRE(sv->act || z_p2, "chained inference edge forward: z must be in the pair layout");
+    const auto kern = nwk == 12 ? (!sv->act ? chain16_fwd_kernel<false, 12, true>
+                                   : z_p2   ? chain16_fwd_kernel<true, 12, true>
+                                            : chain16_fwd_kernel<true, 12, false>)
+                                : (!sv->act ? chain16_fwd_kernel<false, 8, true>
+                                   : z_p2   ? chain16_fwd_kernel<true, 8, true>
+                                            : chain16_fwd_kernel<true, 8, false>);
     const size_t lds = lds_fwd(nwk);
     if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
     ProfScope ps(PROF_FWD_EDGE, st);
@@ -1444,7 +1476,7 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
 
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st) {
+                          hipStream_t st, bool p2) {
     ChainBwdArgs a;
     memset(&a, 0, sizeof(a));
     a.dout = reinterpret_cast<const __bf16*>(dout);
@@ -1468,8 +1500,11 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = 0;
     if (a.ntiles == 0) return 0;
     const int nwk = edge_bwd_waves();
-    const auto kern = nwk == 12 ? (dout ? chain16_bwd_kernel<false, 12> : chain16_bwd_kernel<true, 12>)
-                                : (dout ? chain16_bwd_kernel<false, 8> : chain16_bwd_kernel<true, 8>);
+    const auto kern =
+        nwk == 12 ? (p2 ? (dout ? chain16_bwd_kernel<false, 12, true> : chain16_bwd_kernel<true, 12, true>)
+                        : (dout ? chain16_bwd_kernel<false, 12, false> : chain16_bwd_kernel<true, 12, false>))
+                  : (p2 ? (dout ? chain16_bwd_kernel<false, 8, true> : chain16_bwd_kernel<true, 8, true>)
+                        : (dout ? chain16_bwd_kernel<false, 8, false> : chain16_bwd_kernel<true, 8, false>));
     const size_t lds = lds_bwd(nwk);
     if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
     const int grid = chain16_edge_backward_parts(M);

@@ -1445,12 +1445,15 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 }
 
 // --------------------------------------------------------------------------- host side
+#ifndef MGN_BF16_BM
+#define MGN_BF16_BM 64  // rows per workgroup of the generic bf16 dense / edge kernels (A/B builds: 32)
+#endif
 template <class T>
-constexpr int bm_of() { return sizeof(T) == 4 ? 32 : 64; }
+constexpr int bm_of() { return sizeof(T) == 4 ? 32 : MGN_BF16_BM; }
 // rows per workgroup tile: bf16 node MLPs use 32 (N is ~6x smaller than E: twice the workgroups)
 template <class T, int MODE>
 constexpr int bm_for() { return MODE == MODE_NODE ? 32 : bm_of<T>(); }
-int bm_host(int dtype, int mode) { return dtype == MGN_F32 || mode == MODE_NODE ? 32 : 64; }
+int bm_host(int dtype, int mode) { return dtype == MGN_F32 || mode == MODE_NODE ? 32 : MGN_BF16_BM; }
 
 // Raise a kernel's dynamic-LDS limit once (not per launch: launches may be inside a graph capture).
 int set_lds(const void* fn, size_t bytes) {
@@ -2115,7 +2118,9 @@ __global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
             for (int i = 0; i < G::C::NTW; ++i) {
                 f4 v = g.acc[i][j];
                 if (s == 0 && a.bias0) v += ld4u(a.bias0 + g.n_of(i));
-                const int64_t o = row * (2 * H) + s * H + g.n_of(i);
+                const int n = g.n_of(i);  // 16t + 4g: bf16 P in the chained kernels' pair layout
+                const int64_t o = row * (2 * H) + s * H +
+                                  (a.out_bf16 ? 32 * (n >> 5) + 8 * ((n >> 2) & 3) + 4 * ((n >> 4) & 1) : n);
                 if (a.out_bf16) {
                     const bf16x4 b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
                     *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(a.proj) + o) = b;
@@ -2264,10 +2269,13 @@ int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, cons
     return 0;
 }
 
+#ifndef MGN_COMB_BM
+#define MGN_COMB_BM 16  // rows per node_grad workgroup: 16 (2 segment-sum items per thread) 20.3 -> 18.1 us vs 32
+#endif
 template <class T, int H>
 int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0, const void* dx_part, void* dP8,
                      void* dx, hipStream_t st) {
-    constexpr int BM = bm_for<T, MODE_NODE>(), KSTEP = Mf<T>::KSTEP;
+    constexpr int BM = MGN_COMB_BM, KSTEP = Mf<T>::KSTEP;
     CombArgs a;
     memset(&a, 0, sizeof(a));
     a.dz0 = dz0;
@@ -2444,8 +2452,9 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     ein.proj_i = t->csc_dst;
     ein.proj_j = t->csc_src;
     if (chain) {
-        auto fwd = chain16_edge_forward;
-        if (int r = fwd(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st)) return r;
+        if (int r = chain16_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st,
+                                         chain_node_eligible(node)))
+            return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
                                    nullptr, nullptr, st)) {
         return r;
@@ -2653,8 +2662,9 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
     oe.o2 = c.dz0;
     if (chain_eligible(edge)) {
         int ntiles = 0;
+        // pair-layout z and d_aggr iff the node MLP is chained too (as in the forward)
         if (int r = chain16_edge_backward(edge, E, &saved->edge, de_out, c.d_aggr, t->csc_dst, c.dz8, c.dsp, &ntiles,
-                                          de, c.dz0, st))
+                                          de, c.dz0, st, chain_node_eligible(node)))
             return r;
     } else if (E > 0) {
         if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, c.dz8, c.dsp, st)) return r;
