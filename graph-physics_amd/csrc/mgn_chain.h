@@ -109,9 +109,11 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
 // the block's node MLP is chained too (then the edge z and d_aggr rows are in it as well)
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
                          int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2);
+// din2 / dout2 (p2 only): de_out read / de written in the pair layout (between the edge backwards of
+// consecutive processor blocks, mgn_block_backward_deferred2)
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st, bool p2);
+                          hipStream_t st, bool p2, bool din2 = false, bool dout2 = false);
 // dense MLP in_dim <= 32 -> 128 -> 128 -> 128 -> 128 + RMSNorm, bf16 (the encoders): 16-row chained
 // kernels with the generic DENSE save layout (ReLU masks: chained lane words)
 bool chain_dense_eligible(const mgn_mlp* m);

@@ -557,24 +557,31 @@ struct BIn16 {  // raw bf16: features 16t + 4g .. +3
 
 // ZD: de_out is identically zero (the processor's last block: EncodeProcessDecode returns nodes only)
 // PGA: prefetch the d_aggr gather with the rest (false: the tile loads it itself, 16 VGPRs fewer)
-// P2: z and the d_aggr rows in the pair layout (written by the chained node MLP kernels)
-template <bool ZD, bool P2, bool PGA = true>
+// a row in the accumulator layout: features 16t + 4g .. +3 (P2: stored in the pair layout)
+template <bool P2>
+__device__ __forceinline__ void load_acc_row(u32x2 (&o)[8], const __bf16* row, int g) {
+    if (P2) {
+        load_p2(o, row, g);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) o[t] = *reinterpret_cast<const u32x2*>(row + 16 * t + 4 * g);
+    }
+}
+
+// P2: z and the d_aggr rows in the pair layout (written by the chained node MLP kernels);
+// DIN2: de_out too (written by the next block's edge backward)
+template <bool ZD, bool P2, bool DIN2, bool PGA = true>
 __device__ __forceinline__ void bload(BIn16& in, const ChainBwdArgs& a, int64_t tile, int gi, int lane) {
     const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
-    const int off = 4 * (lane >> 4);
-    const __bf16* d = a.dout + row * H + off;
-    const __bf16* gp = a.gath + (int64_t)gi * H + off;
-    const __bf16* z = a.z_save + row * H + off;
+    const int g = lane >> 4;
+    if (ZD) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        in.d[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
-        if (PGA && !P2) in.ga[t] = *reinterpret_cast<const u32x2*>(gp + 16 * t);
-        if (!P2) in.z[t] = *reinterpret_cast<const u32x2*>(z + 16 * t);
+        for (int t = 0; t < 8; ++t) in.d[t] = u32x2{0u, 0u};
+    } else {
+        load_acc_row<DIN2>(in.d, a.dout + row * H, g);
     }
-    if (P2) {
-        if (PGA) load_p2(in.ga, a.gath + (int64_t)gi * H, lane >> 4);
-        load_p2(in.z, a.z_save + row * H, lane >> 4);
-    }
+    if (PGA) load_acc_row<P2>(in.ga, a.gath + (int64_t)gi * H, g);
+    load_acc_row<P2>(in.z, a.z_save + row * H, g);
     in.q = a.rden_save[row];
 #pragma unroll
     for (int l = 0; l < 3; ++l) in.mask[l] = a.mask32[l * a.mask_stride * 2 + tile * 64 + lane];
@@ -597,7 +604,8 @@ __device__ __forceinline__ void pin_in(const S& in) {
     for (int l = 0; l < 3; ++l) pin(in.mask[l]);
 }
 
-template <bool ZD, int NWK, bool P2>
+// DOUT2: de in the pair layout (for the previous block's edge backward)
+template <bool ZD, int NWK, bool P2, bool DIN2, bool DOUT2>
 __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -616,7 +624,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     int gcur = gi0;
     stage16<4, NWK * 64>(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
-    bload<ZD, P2, PGA>(nxt, a, min(tile, last), gi0, lane);
+    bload<ZD, P2, DIN2, PGA>(nxt, a, min(tile, last), gi0, lane);
     for (int i = threadIdx.x; i < H; i += NWK * 64) vec[i] = a.scale[i];
     __syncthreads();
     // RMSNorm-scale gradient partials of this wave: red[wave][H], one tile at a time (row sums
@@ -682,7 +690,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
 #pragma unroll
         for (int l = 0; l < 3; ++l) mcur[l] = ok ? nxt.mask[l] : 0u;
         STAMP(1);
-        bload<ZD, P2, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
+        bload<ZD, P2, DIN2, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
         bf16x8 B[4];
         to_operand(acc, B);
@@ -691,11 +699,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         u32x2 dre[8];  // de_out of this tile again (cache-hot), for the layer-0 residual
 #pragma unroll
         for (int l = 3; l >= 1; --l) {
-            if (l == 1) {
-                const __bf16* d = a.dout + clamp_row(row, a.M) * H + 4 * g;
-#pragma unroll
-                for (int t = 0; t < 8; ++t) dre[t] = ZD ? u32x2{0u, 0u} : *reinterpret_cast<const u32x2*>(d + 16 * t);
-            }
+            if (l == 1 && !ZD) load_acc_row<DIN2>(dre, a.dout + clamp_row(row, a.M) * H, g);
             // stores its B operand dZ_l (R8) under the MFMAs
             gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
             STAMP(3);
@@ -720,7 +724,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
             }
             gpre = true;
         }
-        store_rows(acc, scr, a.de, tile, a.M, lane);
+        store_rows<DOUT2>(acc, scr, a.de, tile, a.M, lane);
         STAMP(7);
         pin_in<PGA>(nxt);
         pin(ngi2);
@@ -1476,7 +1480,7 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
 
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st, bool p2) {
+                          hipStream_t st, bool p2, bool din2, bool dout2) {
     ChainBwdArgs a;
     memset(&a, 0, sizeof(a));
     a.dout = reinterpret_cast<const __bf16*>(dout);
@@ -1499,12 +1503,17 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.dz0 = reinterpret_cast<__bf16*>(dz0);
     *nparts = 0;
     if (a.ntiles == 0) return 0;
-    const int nwk = edge_bwd_waves();
-    const auto kern =
-        nwk == 12 ? (p2 ? (dout ? chain16_bwd_kernel<false, 12, true> : chain16_bwd_kernel<true, 12, true>)
-                        : (dout ? chain16_bwd_kernel<false, 12, false> : chain16_bwd_kernel<true, 12, false>))
-                  : (p2 ? (dout ? chain16_bwd_kernel<false, 8, true> : chain16_bwd_kernel<true, 8, true>)
-                        : (dout ? chain16_bwd_kernel<false, 8, false> : chain16_bwd_kernel<true, 8, false>));
+    constexpr int nwk = edge_bwd_waves();
+    MGN_REQUIRE(p2 || (!din2 && !dout2), "pair-layout de needs the chained node MLP");
+    using K = void (*)(ChainBwdArgs);
+    const K kern = !p2    ? (dout ? (K)chain16_bwd_kernel<false, nwk, false, false, false>
+                                  : (K)chain16_bwd_kernel<true, nwk, false, false, false>)
+                   : !dout ? (dout2 ? (K)chain16_bwd_kernel<true, nwk, true, false, true>
+                                    : (K)chain16_bwd_kernel<true, nwk, true, false, false>)
+                   : din2  ? (dout2 ? (K)chain16_bwd_kernel<false, nwk, true, true, true>
+                                    : (K)chain16_bwd_kernel<false, nwk, true, true, false>)
+                           : (dout2 ? (K)chain16_bwd_kernel<false, nwk, true, false, true>
+                                    : (K)chain16_bwd_kernel<false, nwk, true, false, false>);
     const size_t lds = lds_bwd(nwk);
     if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
     const int grid = chain16_edge_backward_parts(M);

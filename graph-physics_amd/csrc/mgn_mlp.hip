@@ -2621,12 +2621,15 @@ static int block_bwd_check(const mgn_topology* t, const mgn_mlp* edge, const mgn
 static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
                                     const mgn_block_saved* saved, const void* dx_out, const void* de_out, void* dx,
                                     void* de, float* node_grads, void* ws, size_t ws_bytes, void* keep,
-                                    mgn_stream_t stream) {
+                                    mgn_stream_t stream, int32_t flags = 0) {
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
     const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl, keep);
+    MGN_REQUIRE(!(flags & ~(MGN_BWD_DE_OUT_PAIR | MGN_BWD_DE_PAIR)), "unknown backward layout flags");
+    MGN_REQUIRE(!flags || (chain_eligible(edge) && chain_node_eligible(node)),
+                "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
 
     // node MLP: dY = dx_out -> dx_part = dx_out + dA0[:, :H], d_aggr = dA0[:, H:]
     if (c.chained) {
@@ -2664,7 +2667,8 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         int ntiles = 0;
         // pair-layout z and d_aggr iff the node MLP is chained too (as in the forward)
         if (int r = chain16_edge_backward(edge, E, &saved->edge, de_out, c.d_aggr, t->csc_dst, c.dz8, c.dsp, &ntiles,
-                                          de, c.dz0, st, chain_node_eligible(node)))
+                                          de, c.dz0, st, chain_node_eligible(node), flags & MGN_BWD_DE_OUT_PAIR,
+                                          flags & MGN_BWD_DE_PAIR))
             return r;
     } else if (E > 0) {
         if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, c.dz8, c.dsp, st)) return r;
@@ -2765,12 +2769,22 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
                                 const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
                                 void* dx, void* de, float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                                 void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2, mgn_stream_t stream) {
+    return mgn_block_backward_deferred2(t, edge, node, x, e, saved, dx_out, de_out, dx, de, edge_grads, node_grads, ws,
+                                        ws_bytes, keep, keep_bytes, reduce2, 0, stream);
+}
+
+int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                                 const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                                 void* dx, void* de, float* edge_grads, float* node_grads, void* ws,
+                                 size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
+                                 int32_t flags, mgn_stream_t stream) {
     MGN_REQUIRE(reduce2, "reduce2 (two mgn_wgrad_reduce) required");
     memset(reduce2, 0, 2 * sizeof(mgn_wgrad_reduce));
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     const bool chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
     if (!chained) {  // generic MLPs: reduced at once, nothing left for the caller
+        MGN_REQUIRE(!flags, "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
         if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,
                                              ws_bytes, nullptr, stream))
             return r;
@@ -2779,7 +2793,7 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
     }
     MGN_REQUIRE(keep && keep_bytes >= keep_layout(t, edge, node).total, "block backward keep buffer too small");
     if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
-                                         keep, stream))
+                                         keep, stream, flags))
         return r;
     RedDesc d[2];
     memset(d, 0, sizeof(d));

@@ -13,6 +13,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 MGN_F32 = 0
 MGN_BF16 = 1
+MGN_BWD_DE_OUT_PAIR = 1  # mgn.h: de_out in the pair layout
+MGN_BWD_DE_PAIR = 2      # mgn.h: write de in the pair layout
 MGN_MAX_LAYERS = 8
 
 _vp = ctypes.c_void_p
@@ -96,6 +98,9 @@ EXPORTS = {
     "mgn_block_backward_deferred": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
                                            _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
                                            _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _vp]),
+    "mgn_block_backward_deferred2": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                            _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_wgrad_reduce_many": (_i32, [ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),

@@ -82,6 +82,9 @@ CHAIN_PROJ = True
 # processor blocks' weight-gradient reductions deferred to one launch after the last block
 # (mgn_block_backward_deferred + mgn_wgrad_reduce_many); False: one reduction per block (same sums)
 DEFER_REDUCE = True
+# deferred path: de handed between consecutive blocks' edge backwards in the pair layout
+# (mgn_block_backward_deferred2; bit-identical gradients). MGN_PAIR_DE=0: row-major (A/B timing)
+PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
 _SIDE = {}
 
 
@@ -451,6 +454,10 @@ class EPDFunction(torch.autograd.Function):
         # ONE launch reduces them all after the last block (not when a gradient-ready callback needs
         # each block's gradients as soon as its backward ends)
         defer = DEFER_REDUCE and not overlap and GRAD_READY is None and nb > 0
+        # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides)
+        pair_de = PAIR_DE and defer and de is None and all(
+            L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
+            for b in range(nb))
         if defer:
             kb = max(int(L.mgn_block_backward_keep_bytes(ctypes.byref(topo.struct), ctypes.byref(bdescs[0]),
                                                          ctypes.byref(bdescs[1]))), 256)
@@ -470,10 +477,14 @@ class EPDFunction(torch.autograd.Function):
                     nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
                     ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
             if defer:
-                nat.check(L.mgn_block_backward_deferred(*args, nat.ptr(ws), ws.numel(),
-                                                        ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
-                                                        ctypes.pointer(reds[2 * b]),
-                                                        st))
+                # de between consecutive blocks' edge backwards in the pair layout (the chained kernels'
+                # gather layout); the first block's de stays row-major (the edge encoder / caller read it)
+                flags = 0
+                if pair_de:
+                    flags = (nat.MGN_BWD_DE_OUT_PAIR if b + 1 < nb else 0) | (nat.MGN_BWD_DE_PAIR if b > 0 else 0)
+                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
+                                                         ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
+                                                         ctypes.pointer(reds[2 * b]), flags, st))
             elif not overlap:
                 nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
                 _grad_ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))

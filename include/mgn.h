@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 9
+#define MGN_ABI_VERSION 10
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -217,6 +217,21 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
                                 float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                                 void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                 mgn_stream_t stream);
+/* mgn_block_backward_deferred with row layouts of de_out / de between the edge backwards of
+ * consecutive chained processor blocks (flags; 0 = mgn_block_backward_deferred): the pair layout
+ * stores feature 16t + 4g + r of a row at 32(t>>1) + 8g + 4(t&1) + r (libmgn's gather layout: one
+ * 16-byte load per lane and tile pair). MGN_BWD_DE_OUT_PAIR: de_out is in it (the previous call's de
+ * with MGN_BWD_DE_PAIR); MGN_BWD_DE_PAIR: write de in it. The caller keeps row-major for de_out
+ * handed in from outside and for the de it consumes itself (the first block's, for the edge
+ * encoder). Chained bf16 h=128 edge + node MLPs only (else an error status, mgn_last_error). */
+#define MGN_BWD_DE_OUT_PAIR 1
+#define MGN_BWD_DE_PAIR 2
+int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                                 const void* x, const void* e, const mgn_block_saved* saved,
+                                 const void* dx_out, const void* de_out, void* dx, void* de,
+                                 float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                                 void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
+                                 int32_t flags, mgn_stream_t stream);
 int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream);
 /* The same backward as two calls over one workspace (same arguments): _data writes dx, de (and, for
  * MLPs outside the chained bf16 h=128 kernels, the node-MLP weight gradients); _wgrad then writes the

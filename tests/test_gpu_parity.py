@@ -815,9 +815,11 @@ def test_chained_projection_handoff_matches_per_block_projections(train):
 
 
 def test_deferred_weight_gradient_reduction_is_bitwise_identical():
-    """mgn_block_backward_deferred + mgn_wgrad_reduce_many (every processor block's slab reduction in
+    """mgn_block_backward_deferred2 + mgn_wgrad_reduce_many (every processor block's slab reduction in
     ONE launch after the last block) sums the same slabs in the same fixed order as the per-block
-    reduction: the gradients are bit-identical."""
+    reduction: the gradients are bit-identical. The deferred path also hands de between the blocks'
+    edge backwards in the pair layout (MGN_BWD_DE_*_PAIR) while the per-block path keeps row-major
+    de: the layout moves bits, so the gradients stay bit-identical."""
     from graphphysics.models import _engine
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils import meshes
