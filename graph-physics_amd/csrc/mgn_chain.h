@@ -101,8 +101,10 @@ bool chain_node_eligible(const mgn_mlp* m);  // bf16, 256 -> 128 -> 128, 4 layer
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
                          hipStream_t st, const mgn_mlp* next_edge = nullptr, void* next_proj = nullptr);
+// din2: dout (dx_out) in the pair layout (mgn_block_backward_deferred2, MGN_BWD_DX_OUT_PAIR)
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
-                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st);
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st,
+                          bool din2 = false);
 // edge MLP forward / backward: 16x16x32 tiles, 12 waves per workgroup (three per SIMD);
 // nparts: number of dscale partial rows written (the reduction's row count)
 // Pair layout (mgn_chain16.hip col_of): the bf16 node projections P are always in it; z_p2 / p2 =

@@ -977,6 +977,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     STAMP_PRINT("nfwd16");
 }
 
+// DIN2: dx_out in the pair layout (written by the next block's node_grad)
+template <bool DIN2>
 __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -997,9 +999,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         const bool ok = row < a.M;
         const int64_t v = clamp_row(row, a.M);
         u32x2 zr[8];
-        const __bf16* dp = a.dout + v * H + 4 * g;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) d[t] = *reinterpret_cast<const u32x2*>(dp + 16 * t);
+        load_acc_row<DIN2>(d, a.dout + v * H, g);
         load_p2(zr, a.z_save + v * H, g);  // the node forward's z: pair layout
         const float qd = a.rden_save[v];
 #pragma unroll
@@ -1586,7 +1586,7 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
 }
 
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
-                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st) {
+                          float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st, bool din2) {
     ChainNodeBwdArgs a;
     memset(&a, 0, sizeof(a));
     a.dout = reinterpret_cast<const __bf16*>(dout);
@@ -1607,11 +1607,12 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.d_aggr = reinterpret_cast<__bf16*>(d_aggr);
     *nparts = 0;
     if (M == 0) return 0;
-    if (int e2 = set_lds_once((const void*)chain16_node_bwd_kernel, LDS_TOTAL)) return e2;
+    const auto kern = din2 ? chain16_node_bwd_kernel<true> : chain16_node_bwd_kernel<false>;
+    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
     const int grid = chain16_node_backward_parts(M);
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
-    hipLaunchKernelGGL(chain16_node_bwd_kernel, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

@@ -2143,6 +2143,7 @@ struct CombArgs {
     void* dx;             // [N][H] (T)
     int64_t N, RP;
     int32_t ldb, HP, NS;
+    int32_t dx_pair;      // dx in the chained kernels' pair layout (bf16 h=128)
 };
 
 template <class T, int H, int BM>
@@ -2225,8 +2226,9 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
         if (row >= a.N) continue;
 #pragma unroll
         for (int i = 0; i < G::C::NTW; ++i) {
-            const int n = g.n_of(i);
-            st4(dx + row * H + n, ld4(dxp + row * H + n) + g.acc[i][j]);
+            const int n = g.n_of(i);  // 16t + 4g (pair layout: 32(t>>1) + 8g + 4(t&1))
+            const int nd = a.dx_pair ? 32 * (n >> 5) + 8 * ((n >> 2) & 3) + 4 * ((n >> 4) & 1) : n;
+            st4(dx + row * H + nd, ld4(dxp + row * H + n) + g.acc[i][j]);
         }
     }
 }
@@ -2274,7 +2276,7 @@ int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, cons
 #endif
 template <class T, int H>
 int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0, const void* dx_part, void* dP8,
-                     void* dx, hipStream_t st) {
+                     void* dx, hipStream_t st, bool dx_pair = false) {
     constexpr int BM = MGN_COMB_BM, KSTEP = Mf<T>::KSTEP;
     CombArgs a;
     memset(&a, 0, sizeof(a));
@@ -2286,6 +2288,7 @@ int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0
     a.wt0 = edge->wtpack;
     a.dP8 = dP8;
     a.dx = dx;
+    a.dx_pair = dx_pair && H == 128 && sizeof(T) == 2;
     a.N = t->num_nodes;
     a.RP = rows_pad(a.N);
     a.HP = rup(H, KSTEP);
@@ -2627,7 +2630,8 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
     const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl, keep);
-    MGN_REQUIRE(!(flags & ~(MGN_BWD_DE_OUT_PAIR | MGN_BWD_DE_PAIR)), "unknown backward layout flags");
+    MGN_REQUIRE(!(flags & ~(MGN_BWD_DE_OUT_PAIR | MGN_BWD_DE_PAIR | MGN_BWD_DX_OUT_PAIR | MGN_BWD_DX_PAIR)),
+                "unknown backward layout flags");
     MGN_REQUIRE(!flags || (chain_eligible(edge) && chain_node_eligible(node)),
                 "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
 
@@ -2637,7 +2641,7 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, t->num_nodes), "backward workspace too small");
         int nparts = 0;
         if (int r = chain16_node_backward(node, t->num_nodes, &saved->node, dx_out, c.ndz, c.ndsp, &nparts, c.dx_part,
-                                          c.d_aggr, st))
+                                          c.d_aggr, st, flags & MGN_BWD_DX_OUT_PAIR))
             return r;
     } else {
         MlpIn nin;
@@ -2678,7 +2682,8 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
     if (dt == MGN_F32) {
         MGN_DISPATCH_H(H, rc = (launch_node_grad<float, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st)))
     } else {
-        MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st)))
+        MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st,
+                                                              flags & MGN_BWD_DX_PAIR)))
     }
     return rc;
 }

@@ -15,6 +15,8 @@ MGN_F32 = 0
 MGN_BF16 = 1
 MGN_BWD_DE_OUT_PAIR = 1  # mgn.h: de_out in the pair layout
 MGN_BWD_DE_PAIR = 2      # mgn.h: write de in the pair layout
+MGN_BWD_DX_OUT_PAIR = 4  # mgn.h: dx_out in the pair layout
+MGN_BWD_DX_PAIR = 8      # mgn.h: write dx in the pair layout
 MGN_MAX_LAYERS = 8
 
 _vp = ctypes.c_void_p

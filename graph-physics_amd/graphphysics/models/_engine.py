@@ -82,7 +82,7 @@ CHAIN_PROJ = True
 # processor blocks' weight-gradient reductions deferred to one launch after the last block
 # (mgn_block_backward_deferred + mgn_wgrad_reduce_many); False: one reduction per block (same sums)
 DEFER_REDUCE = True
-# deferred path: de handed between consecutive blocks' edge backwards in the pair layout
+# deferred path: de / dx handed between consecutive blocks in the pair layout
 # (mgn_block_backward_deferred2; bit-identical gradients). MGN_PAIR_DE=0: row-major (A/B timing)
 PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
 _SIDE = {}
@@ -477,11 +477,14 @@ class EPDFunction(torch.autograd.Function):
                     nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
                     ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
             if defer:
-                # de between consecutive blocks' edge backwards in the pair layout (the chained kernels'
-                # gather layout); the first block's de stays row-major (the edge encoder / caller read it)
+                # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
+                # layout); the first block's stay row-major (the encoders / the caller read them)
                 flags = 0
                 if pair_de:
-                    flags = (nat.MGN_BWD_DE_OUT_PAIR if b + 1 < nb else 0) | (nat.MGN_BWD_DE_PAIR if b > 0 else 0)
+                    if b + 1 < nb:
+                        flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
+                    if b > 0:
+                        flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
                                                          ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
                                                          ctypes.pointer(reds[2 * b]), flags, st))

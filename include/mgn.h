@@ -217,15 +217,18 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
                                 float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
                                 void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                 mgn_stream_t stream);
-/* mgn_block_backward_deferred with row layouts of de_out / de between the edge backwards of
- * consecutive chained processor blocks (flags; 0 = mgn_block_backward_deferred): the pair layout
- * stores feature 16t + 4g + r of a row at 32(t>>1) + 8g + 4(t&1) + r (libmgn's gather layout: one
- * 16-byte load per lane and tile pair). MGN_BWD_DE_OUT_PAIR: de_out is in it (the previous call's de
- * with MGN_BWD_DE_PAIR); MGN_BWD_DE_PAIR: write de in it. The caller keeps row-major for de_out
- * handed in from outside and for the de it consumes itself (the first block's, for the edge
- * encoder). Chained bf16 h=128 edge + node MLPs only (else an error status, mgn_last_error). */
+/* mgn_block_backward_deferred with row layouts of the gradients handed between consecutive chained
+ * processor blocks (flags; 0 = mgn_block_backward_deferred): the pair layout stores feature
+ * 16t + 4g + r of a row at 32(t>>1) + 8g + 4(t&1) + r (libmgn's gather layout: one 16-byte load per
+ * lane and tile pair). MGN_BWD_DE_OUT_PAIR / MGN_BWD_DX_OUT_PAIR: de_out / dx_out are in it (the
+ * previous call's de / dx written with MGN_BWD_DE_PAIR / MGN_BWD_DX_PAIR). The caller keeps
+ * row-major for gradients handed in from outside and for the de / dx it consumes itself (the first
+ * block's, for the encoders). Chained bf16 h=128 edge + node MLPs only (else an error status,
+ * mgn_last_error). */
 #define MGN_BWD_DE_OUT_PAIR 1
 #define MGN_BWD_DE_PAIR 2
+#define MGN_BWD_DX_OUT_PAIR 4
+#define MGN_BWD_DX_PAIR 8
 int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
                                  const void* x, const void* e, const mgn_block_saved* saved,
                                  const void* dx_out, const void* de_out, void* dx, void* de,
