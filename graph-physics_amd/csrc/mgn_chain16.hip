@@ -1,7 +1,7 @@
 // Register-chained edge-MLP kernels on 16-row tiles (v_mfma_f32_16x16x32_bf16), bf16, h=128.
 //
-// Same structure as mgn_chain.hip (one wave runs the whole 4-Linear chain of its edges, weights
-// resident in LDS, accumulators chained as the next layer's B operand), on 16x16x32 tiles: a wave
+// One wave runs the whole 4-Linear chain of its edges (weights resident in LDS, accumulators
+// chained as the next layer's B operand), on 16x16x32 tiles: a wave
 // owns 16 edges, its accumulator is 8 f32x4 (32 VGPRs) instead of 64, so TWO waves fit per SIMD
 // (8 waves per workgroup share one 128 KiB weight image) and one wave's epilogue VALU overlaps the
 // other's MFMAs and memory traffic.
@@ -115,7 +115,7 @@ __device__ __forceinline__ float row16_sum4(const f4& v, int m) {
 
 __device__ __forceinline__ int64_t clamp_row(int64_t row, int64_t M) { return row < M ? row : M - 1; }
 
-// w = 2w + (v > 0) (see mgn_chain.hip)
+// w = 2w + (v > 0): v_cmp sets vcc, v_addc shifts it in (2 instructions, no constants)
 __device__ __forceinline__ unsigned push_bit(unsigned w, float v) {
     unsigned r;
     asm("v_cmp_lt_f32 vcc, 0, %2\n\tv_addc_co_u32 %0, vcc, %1, %1, vcc" : "=v"(r) : "v"(w), "v"(v) : "vcc");
