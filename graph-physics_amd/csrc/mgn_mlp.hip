@@ -2242,10 +2242,13 @@ void proj_window(int H, int s, int* ks0, int* nks, int* off) {
     *off = s * H - *ks0 * KSTEP;
 }
 
+#ifndef MGN_PROJ_BM
+#define MGN_PROJ_BM 32  // rows per node_proj workgroup (A/B builds: 16)
+#endif
 template <class T, int H>
 int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, const float* bias0, hipStream_t st,
                 bool out_bf16 = false) {
-    constexpr int BM = bm_for<T, MODE_NODE>(), KSTEP = Mf<T>::KSTEP;
+    constexpr int BM = MGN_PROJ_BM, KSTEP = Mf<T>::KSTEP;
     ProjArgs a;
     memset(&a, 0, sizeof(a));
     a.x = x;
@@ -2796,7 +2799,14 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
         return block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,
                                          nullptr, nullptr, stream);
     }
-    MGN_REQUIRE(keep && keep_bytes >= keep_layout(t, edge, node).total, "block backward keep buffer too small");
+    if (!keep) {  // reduced at once (mgn_block_backward with layout flags): reduce2 stays zeroed
+        if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,
+                                             ws_bytes, nullptr, stream, flags))
+            return r;
+        return block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,
+                                         nullptr, nullptr, stream);
+    }
+    MGN_REQUIRE(keep_bytes >= keep_layout(t, edge, node).total, "block backward keep buffer too small");
     if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
                                          keep, stream, flags))
         return r;

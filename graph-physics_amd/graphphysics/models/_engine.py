@@ -455,7 +455,7 @@ class EPDFunction(torch.autograd.Function):
         # each block's gradients as soon as its backward ends)
         defer = DEFER_REDUCE and not overlap and GRAD_READY is None and nb > 0
         # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides)
-        pair_de = PAIR_DE and defer and de is None and all(
+        pair_de = PAIR_DE and not overlap and de is None and all(
             L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
             for b in range(nb))
         if defer:
@@ -476,20 +476,25 @@ class EPDFunction(torch.autograd.Function):
                     nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
                     nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
                     ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
+            # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
+            # layout); the first block's stay row-major (the encoders / the caller read them)
+            flags = 0
+            if pair_de:
+                if b + 1 < nb:
+                    flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
+                if b > 0:
+                    flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
             if defer:
-                # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
-                # layout); the first block's stay row-major (the encoders / the caller read them)
-                flags = 0
-                if pair_de:
-                    if b + 1 < nb:
-                        flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
-                    if b > 0:
-                        flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
                                                          ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
                                                          ctypes.pointer(reds[2 * b]), flags, st))
             elif not overlap:
-                nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
+                if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
+                    red2 = (nat.WgradReduce * 2)()
+                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(), None, 0, red2, flags,
+                                                             st))
+                else:
+                    nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
                 _grad_ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
             else:
                 w = wss[b % 2]

@@ -224,7 +224,8 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
  * previous call's de / dx written with MGN_BWD_DE_PAIR / MGN_BWD_DX_PAIR). The caller keeps
  * row-major for gradients handed in from outside and for the de / dx it consumes itself (the first
  * block's, for the encoders). Chained bf16 h=128 edge + node MLPs only (else an error status,
- * mgn_last_error). */
+ * mgn_last_error). keep = NULL: nothing deferred — the block's weight gradients are reduced at once
+ * (mgn_block_backward with the layout flags; reduce2 zeroed). */
 #define MGN_BWD_DE_OUT_PAIR 1
 #define MGN_BWD_DE_PAIR 2
 #define MGN_BWD_DX_OUT_PAIR 4

@@ -817,9 +817,9 @@ def test_chained_projection_handoff_matches_per_block_projections(train):
 def test_deferred_weight_gradient_reduction_is_bitwise_identical():
     """mgn_block_backward_deferred2 + mgn_wgrad_reduce_many (every processor block's slab reduction in
     ONE launch after the last block) sums the same slabs in the same fixed order as the per-block
-    reduction: the gradients are bit-identical. The deferred path also hands de between the blocks'
-    edge backwards in the pair layout (MGN_BWD_DE_*_PAIR) while the per-block path keeps row-major
-    de: the layout moves bits, so the gradients stay bit-identical."""
+    reduction: the gradients are bit-identical. The hand-offs of de / dx between consecutive blocks in
+    the pair layout (MGN_BWD_*_PAIR, also on the per-block path with keep = NULL) only move bits:
+    bit-identical to row-major hand-offs."""
     from graphphysics.models import _engine
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils import meshes
@@ -831,14 +831,16 @@ def test_deferred_weight_gradient_reduction_is_bitwise_identical():
     torch.manual_seed(0)
     m = EncodeProcessDecode(4, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
     grads = []
-    for defer in (True, False):
-        _engine.DEFER_REDUCE = defer
+    # deferred + pair-layout hand-offs, per-block reduction + pair layout, per-block + row-major
+    for defer, pair in ((True, True), (False, True), (False, False)):
+        _engine.DEFER_REDUCE, _engine.PAIR_DE = defer, pair
         try:
             y = m(g)
             y.backward(torch.ones_like(y))
             grads.append([p.grad.clone() for p in m.parameters()])
             m.zero_grad(set_to_none=True)
         finally:
-            _engine.DEFER_REDUCE = True
-    for a, c in zip(*grads):
-        assert torch.equal(a, c)
+            _engine.DEFER_REDUCE, _engine.PAIR_DE = True, True
+    for other in grads[1:]:
+        for a, c in zip(grads[0], other):
+            assert torch.equal(a, c)
