@@ -82,6 +82,9 @@ CHAIN_PROJ = True
 # processor blocks' weight-gradient reductions deferred to one launch after the last block
 # (mgn_block_backward_deferred + mgn_wgrad_reduce_many); False: one reduction per block (same sums)
 DEFER_REDUCE = True
+# data-parallel backward: processor blocks reduced (and handed to GRAD_READY) in groups of about this
+# many gradient bytes — one reduction launch per all-reduce bucket instead of one per block
+GRAD_GROUP_BYTES = 4 << 20
 # deferred path: de / dx handed between consecutive blocks in the pair layout
 # (mgn_block_backward_deferred2; bit-identical gradients). MGN_PAIR_DE=0: row-major (A/B timing)
 PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
@@ -451,9 +454,11 @@ class EPDFunction(torch.autograd.Function):
         # reused only after the side stream has finished with it). Joined before returning.
         overlap = OVERLAP_WGRAD and nb > 1
         # deferred weight-gradient reductions: each block leaves its slabs in its own keep buffer and
-        # ONE launch reduces them all after the last block (not when a gradient-ready callback needs
-        # each block's gradients as soon as its backward ends)
-        defer = DEFER_REDUCE and not overlap and GRAD_READY is None and nb > 0
+        # ONE launch reduces them all after the last block; with a gradient-ready callback (the
+        # data-parallel bucketed all-reduce) one launch per group of blocks whose gradients fill a
+        # bucket (GRAD_GROUP_BYTES), handed over as one range as soon as the group's backward ends
+        defer = DEFER_REDUCE and not overlap and nb > 0
+        pend_hi = pend_b = None  # open group: the range end of its first (highest) block, that block
         # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides)
         pair_de = PAIR_DE and not overlap and de is None and all(
             L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
@@ -488,6 +493,16 @@ class EPDFunction(torch.autograd.Function):
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
                                                          ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
                                                          ctypes.pointer(reds[2 * b]), flags, st))
+                if GRAD_READY is not None:
+                    if pend_hi is None:
+                        pend_b = b
+                        pend_hi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
+                    if (pend_hi - boff[2 * b]) * 4 >= GRAD_GROUP_BYTES or b == 0:
+                        # blocks b..pend_b: consecutive descriptors from reds[2b]
+                        nat.check(L.mgn_wgrad_reduce_many(ctypes.byref(reds, 2 * b * ctypes.sizeof(nat.WgradReduce)),
+                                                          2 * (pend_b - b + 1), st))
+                        _grad_ready(G, boff[2 * b], pend_hi)
+                        pend_hi = pend_b = None
             elif not overlap:
                 if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
                     red2 = (nat.WgradReduce * 2)()
@@ -509,7 +524,7 @@ class EPDFunction(torch.autograd.Function):
                 ev.record(side)
                 done[b % 2] = ev
             dx, de = dx1, de1
-        if defer:
+        if defer and GRAD_READY is None:
             nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
         if overlap:
             for ev in done:
