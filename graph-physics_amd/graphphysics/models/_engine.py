@@ -459,8 +459,9 @@ class EPDFunction(torch.autograd.Function):
         # bucket (GRAD_GROUP_BYTES), handed over as one range as soon as the group's backward ends
         defer = DEFER_REDUCE and not overlap and nb > 0
         pend_hi = pend_b = None  # open group: the range end of its first (highest) block, that block
-        # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides)
-        pair_de = PAIR_DE and not overlap and de is None and all(
+        # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides;
+        # a graph without edges or nodes runs the generic kernels: row-major)
+        pair_de = PAIR_DE and not overlap and de is None and N > 0 and E > 0 and all(
             L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
             for b in range(nb))
         if defer:

@@ -316,6 +316,28 @@ def test_empty_edge_set():
     assert relerr(y, yr) < 1e-4
 
 
+def test_empty_edge_set_bf16_training():
+    """bf16 h=128 (the chained kernels' shape) on a graph without edges, forward and backward: the
+    blocks fall back to the generic kernels where a side is empty, so the backward hands de / dx
+    row-major (no pair layout); gradients are finite and the output matches the oracle."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(3, 5, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
+    x = torch.randn(40, 5)
+    g = Data(x=x.to(DEV), edge_index=torch.zeros((2, 0), dtype=torch.long, device=DEV),
+             edge_attr=torch.zeros((0, 3), device=DEV))
+    y = m(g)
+    y.backward(torch.ones_like(y))
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+    torch.manual_seed(0)
+    ref = O.OracleEPD(3, 5, 3, 2, 128)
+    yr = O.encode_process_decode(x, torch.zeros((2, 0), dtype=torch.long), torch.zeros((0, 3)),
+                                 dict(ref.named_parameters()), 3)
+    assert relerr(y, yr) < 5e-2
+
+
 def test_encoder_input_gradients():
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils.data import Data
