@@ -228,7 +228,11 @@ def main():
     prof = {}
     if not a.no_profile:
         # Per-kernel durations: HIP events on the launch stream around every kernel of K more steps
-        # run eagerly (the same kernels, shapes and launch order the replayed graph contains).
+        # run eagerly (the same kernels, shapes and launch order the replayed graph contains), after
+        # two unprofiled eager steps (the first eager step after the replays pays one-time costs).
+        for _ in range(2):
+            step.eager()
+        torch.cuda.synchronize()
         nat.profile_enable(True)
         for _ in range(a.steps):
             step.eager()
