@@ -214,7 +214,6 @@ def main():
         # a new Batch per step, as the Lightning loop collates: new tensors (topology cache miss)
         for k, v in base.items():
             setattr(data, k, v.clone())
-        step.node_type = data.x[:, step.sim.node_type_index]
 
     t0 = time.perf_counter()
     for _ in range(a.steps):

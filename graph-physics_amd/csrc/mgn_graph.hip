@@ -110,8 +110,18 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         const double* __restrict__ hyper, double beta1,
-                                                        double beta2, double eps, double wd) {
+                                                        double beta2, double eps, double wd, unsigned* err) {
 #pragma clang fp contract(off)
+    if (err) {  // a pending validation error: the reference raised before its optimizer step
+        const unsigned e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e & MGN_ERR_ANY) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                if ((e & MGN_ERR_SKIP_MASK) != MGN_ERR_SKIP_MASK) atomicAdd(err, MGN_ERR_SKIP_ONE);
+                atomicOr(err, MGN_ERR_STALE);
+            }
+            return;
+        }
+    }
     const double lr = hyper[0], step = hyper[1];
     const double bc1 = 1.0 - pow(beta1, step), bc2 = 1.0 - pow(beta2, step);
     const float decay = (float)(1.0 - lr * wd), w1 = (float)(1.0 - beta1), b2 = (float)beta2;
@@ -213,11 +223,14 @@ __device__ __forceinline__ void normalizer_update_body(const float* __restrict__
                                                        const float* __restrict__ pending, float rows_f,
                                                        int accumulate, float* acc_sum, float* acc_sum_sq,
                                                        float* acc_count, float* num_acc, float max_acc, float eps,
-                                                       float* __restrict__ mstd) {
+                                                       float* __restrict__ mstd, bool skip = false) {
 #pragma clang fp contract(off)  // one rounding per torch op: no fused multiply-adds here
     __shared__ float tot[2 * 32];
     const int i = threadIdx.x;
     const float count_old = *acc_count, num_old = *num_acc;
+    // skip: a validation error is pending on the device word — the reference raised before this
+    // normalizer accumulated, so the buffers stay as they are (the outputs are never used)
+    if (skip) accumulate = 0;
     if (accumulate && !pending)
         for (int o = threadIdx.x >> 6; o < 2 * cols; o += 4) {
             const float t = partial_total(part, nblocks, cols, o, threadIdx.x & 63);
@@ -345,10 +358,20 @@ __global__ __launch_bounds__(256) void preamble_stats(PreArgs a) {
     if (threadIdx.x < 2 * cols) q.part[b * 2 * cols + threadIdx.x] = red[threadIdx.x][0];
 }
 
+__device__ __forceinline__ unsigned load_err(const unsigned* err) {
+    return err ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+}
+
 __global__ __launch_bounds__(256) void preamble_update(PreArgs a) {
     const PreSrc& q = a.s[blockIdx.x];
+    // reference order (simulator.py _build_input_graph): the output normalizer accumulates, THEN
+    // F.one_hot validates the node types, then the node / edge normalizers accumulate. An error of
+    // THIS step (type bits set by preamble_stats, or an earlier unraised one) stops the node / edge
+    // updates; the output normalizer stops only for an error of an earlier step (MGN_ERR_STALE).
+    const unsigned e = load_err(a.err);
+    const bool skip = blockIdx.x == 0 ? (e & MGN_ERR_STALE) != 0u : (e & (MGN_ERR_ANY | MGN_ERR_STALE)) != 0u;
     normalizer_update_body(q.part, q.nb, q.cols, q.pending, (float)q.rows, a.accumulate, q.acc_sum, q.acc_sum_sq,
-                           q.acc_count, q.num_acc, q.max_acc, q.eps, q.mstd);
+                           q.acc_count, q.num_acc, q.max_acc, q.eps, q.mstd, skip);
 }
 
 // batch statistics only (the data-parallel prologue): per source {Σx, Σx², rows}, packed in source
@@ -471,13 +494,13 @@ extern "C" {
 
 int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
-                  mgn_stream_t stream) {
+                  uint32_t* err_word, mgn_stream_t stream) {
     if (n == 0) return 0;
     int64_t blocks = cdiv64(cdiv64(n, 4), 256);
     if (blocks > 512) blocks = 512;
     ProfScope ps(PROF_ADAMW, (hipStream_t)stream);
     hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                       exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay);
+                       exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay, (unsigned*)err_word);
     MGN_LAUNCH_CHECK();
     return 0;
 }

@@ -1882,11 +1882,13 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     };
     // one round of workgroups, every one over about the same number of rows: 4 edge jobs on ce
     // chunks, 5 node jobs on cn chunks, the 2 W0-projection jobs (node rows, into the edge slabs'
-    // x-block columns) on cp = cn chunks — the reduction sums only the first cp slabs of those
-    // columns (RedDesc x-columns), so the projections need not be cut into ce short chunks
+    // x-block columns) on cp ≈ cn chunks — the reduction sums only the first cp slabs of those
+    // columns (RedDesc x-columns), so the projections need not be cut into ce short chunks. The
+    // edge slab buffer holds wgrad_max_chunks(RPE) slabs (keep_layout, mlp_bwd_ws): cp is capped
+    // there (graphs with more nodes than edges).
     const int cus = device_cus();
     int ce = 1, cn = 1, cp = 1;
-    int re = 0, rn = 0;
+    int re = 0, rn = 0, rp = 0;
     {
         const int64_t total = 4 * RPE + 7 * RPN;
         for (int64_t target = cdiv64(cdiv64(total, cus), 64) * 64;; target += 64) {
@@ -1894,9 +1896,11 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
             rn = rows_for(RPN, target, &cn);
             if (4 * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
         }
-        cp = cn;
+        const int64_t cpmax = wgrad_max_chunks(RPE);
+        const int64_t c = cn < cpmax ? cn : cpmax;
+        rp = (int)(cdiv64(cdiv64(RPN, c), 64) * 64);
+        cp = (int)cdiv64(RPN, rp);
     }
-    const int rp = rn;
     RgArgs r;
     memset(&r, 0, sizeof(r));
     int nj = 0, wg = 0;

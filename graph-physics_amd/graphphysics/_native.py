@@ -10,6 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
+ABI_VERSION = 11  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -122,7 +123,7 @@ EXPORTS = {
     "mgn_masked_mse": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp, _sz, _vp]),
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
-    "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+    "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp, _vp]),
     "mgn_coalesce_workspace_bytes": (_sz, [_i64]),
     "mgn_coalesce": (_i32, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _sz, _vp]),
     "mgn_face_to_edge_keys": (_i64, [_i32, _i64]),
@@ -172,6 +173,9 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mgn_abi_version() != ABI_VERSION:  # a stale build would mis-read changed signatures
+        raise RuntimeError(f"libmgn ABI {lib.mgn_abi_version()} at {path}, these bindings need {ABI_VERSION}: "
+                           "rebuild (python __graft_entry__.py)")
     _lib = lib
     return lib
 
@@ -190,17 +194,24 @@ def check(rc):
 
 # ---------------------------------------------------------------- device error word (ABI v7)
 ERR_EDGE_INDEX, ERR_TYPE_NEG, ERR_TYPE_BIG = 1, 2, 4
+ERR_ANY, ERR_SKIP_SHIFT, ERR_STALE = 0xFFFF, 16, 1 << 31  # ABI v11 (include/mgn.h)
 
 
 def _raise_for(bits):
-    """The exception the reference raises for the validation failure in `bits`."""
+    """The exception the reference raises for the validation failure in `bits`. The exception's
+    `mgn_skipped_updates` is the number of optimizer steps mgn_adamw_dev skipped because the error
+    was pending (the caller rewinds its host-side step counters by as many)."""
+    ex = None
     if bits & ERR_EDGE_INDEX:
-        raise IndexError("edge_index out of range: an index is outside [0, num_nodes) "
-                         "(libmgn device check; the reference's ATen gather raises IndexError)")
-    if bits & ERR_TYPE_NEG:
-        raise RuntimeError("Class values must be non-negative.")  # F.one_hot (reference simulator one-hot)
-    if bits & ERR_TYPE_BIG:
-        raise RuntimeError("Class values must be smaller than num_classes.")
+        ex = IndexError("edge_index out of range: an index is outside [0, num_nodes) "
+                        "(libmgn device check; the reference's ATen gather raises IndexError)")
+    elif bits & ERR_TYPE_NEG:
+        ex = RuntimeError("Class values must be non-negative.")  # F.one_hot (reference simulator one-hot)
+    elif bits & ERR_TYPE_BIG:
+        ex = RuntimeError("Class values must be smaller than num_classes.")
+    if ex is not None:
+        ex.mgn_skipped_updates = (bits >> ERR_SKIP_SHIFT) & 0xFF
+        raise ex
 
 
 class ErrorWord:

@@ -50,24 +50,37 @@ class Simulator(nn.Module):
                 if n is not None]
 
     @torch.no_grad()
-    def exchange_statistics(self, inputs, group=None):
+    def exchange_statistics(self, inputs, group=None, loss_masks=None):
         """Data-parallel prologue for a replayed step: the batch statistics of all three normalizers
         (the same inputs the training forward accumulates) in ONE packed all-reduce over `group`,
         parked with Normalizer.set_pending() for the next forward. They depend only on the batch, so
-        exchanging them before the (captured) forward is exact."""
+        exchanging them before the (captured) forward is exact.
+
+        loss_masks (node types of the masked L2 loss): the batch's masked-node count rides in the
+        same all-reduce (one extra float); returns the GLOBAL count as a 1-element device tensor at a
+        stable address (a captured loss reads the current batch's count from it), else None."""
         import torch.distributed as dist
+
+        from graphphysics.utils.loss import _prepare_mask_for_loss
+
+        def local_count(dst):
+            if loss_masks is None:
+                dst.zero_()
+                return
+            nt = inputs.x[:, self.node_type_index]
+            dst.copy_(_prepare_mask_for_loss(nt[:, None], nt, list(loss_masks)).sum(dtype=torch.float32).reshape(1))
 
         if self._fused_preamble_ok(inputs, False):
             # one libmgn pass writes every normalizer's {Σx, Σx², count} into one buffer the
-            # normalizers' pending statistics are views of: one all-reduce, no copies
+            # normalizers' pending statistics are views of (+ the loss count): one all-reduce, no copies
             from graphphysics import _native as nat
 
             norms = self.normalizers()
             sizes = [2 * n._acc_sum.numel() + 1 for n in norms]
             buf = getattr(self, "_stats_buf", None)
-            if buf is None or buf.numel() != sum(sizes) or buf.device != inputs.x.device or \
+            if buf is None or buf.numel() != sum(sizes) + 1 or buf.device != inputs.x.device or \
                     any(n._pending_packed is None for n in norms):
-                buf = torch.zeros(sum(sizes), dtype=torch.float32, device=inputs.x.device)
+                buf = torch.zeros(sum(sizes) + 1, dtype=torch.float32, device=inputs.x.device)
                 o = 0
                 for n, k in zip(norms, sizes):
                     n.bind_pending(buf[o:o + k])
@@ -77,19 +90,22 @@ class Simulator(nn.Module):
                                      inputs.edge_attr if self._edge_normalizer is not None else None,
                                      (self.feature_index_start, self.feature_index_end),
                                      (self.output_index_start, self.output_index_end), self.node_type_index,
-                                     NodeType.SIZE, buf)
+                                     NodeType.SIZE, buf[:-1])
+            local_count(buf[-1:])
             if dist.is_available() and dist.is_initialized():
                 dist.all_reduce(buf, group=group)
             for n in norms:
                 n.mark_pending_fresh()
-            return
+            return buf[-1:] if loss_masks is not None else None
         delta = inputs.y - self._get_pre_target(inputs)
         nf = self._build_node_features(inputs, self._get_one_hot_type(inputs))
         srcs = [(self._output_normalizer, delta), (self._node_normalizer, nf)]
         if self._edge_normalizer is not None:
             srcs.append((self._edge_normalizer, inputs.edge_attr))
         stats = [n.batch_statistics(d) for n, d in srcs]
-        packed = torch.cat([t.reshape(-1).float() for st in stats for t in st])
+        cnt = torch.zeros(1, dtype=torch.float32, device=inputs.x.device)
+        local_count(cnt)
+        packed = torch.cat([t.reshape(-1).float() for st in stats for t in st] + [cnt])
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(packed, group=group)
         o = 0
@@ -97,6 +113,14 @@ class Simulator(nn.Module):
             k = s.numel()
             n.set_pending(packed[o:o + k].view_as(s), packed[o + k:o + 2 * k].view_as(s2), packed[o + 2 * k])
             o += 2 * k + 1
+        if loss_masks is None:
+            return None
+        # a stable address for callers that capture the loss (the packed tensor is new each call)
+        cb = getattr(self, "_count_buf", None)
+        if cb is None or cb.device != packed.device:
+            cb = self._count_buf = torch.zeros(1, dtype=torch.float32, device=packed.device)
+        cb.copy_(packed[-1:])
+        return cb
 
     def _get_pre_target(self, inputs) -> torch.Tensor:
         return inputs.x[:, self.output_index_start:self.output_index_end]

@@ -32,6 +32,19 @@ def global_masked_mse(target, network_output, node_type, masks, group=None, coun
     return masked_mse(target, network_output, node_type, masks, count=count)
 
 
+def sum_allreduce_hook(process_group, bucket):
+    """DistributedDataParallel communication hook that SUMS gradient buckets over ranks (DDP's
+    default hook averages them). With global_masked_mse — whose per-rank losses SUM to the global
+    masked mean — the summed gradients are exactly the single-process gradients on the union batch;
+    averaged ones would be 1/world_size of them. Register it on the Lightning / DDP path:
+        ddp_model.register_comm_hook(None, sum_allreduce_hook)
+        # Lightning: Trainer(strategy=DDPStrategy(ddp_comm_hook=sum_allreduce_hook), ...)
+    """
+    group = process_group if process_group is not None else dist.group.WORLD
+    fut = dist.all_reduce(bucket.buffer(), group=group, async_op=True).get_future()
+    return fut.then(lambda f: f.value()[0])
+
+
 def flat_grad_buffer(params):
     """The single contiguous tensor all gradients are views of, or None."""
     gs = [p.grad for p in params if p.grad is not None]
@@ -108,8 +121,12 @@ class GradBuckets:
             self.comm = torch.cuda.Stream(device=G.device)
         self.comm.wait_stream(cur)
         with torch.cuda.stream(self.comm):
-            dist.all_reduce(G[lo:hi], group=self.group)
+            self._reduce(G[lo:hi])
         self.issued += 1
+
+    def _reduce(self, t):
+        """The in-place collective of one bucket, issued on the communication stream."""
+        dist.all_reduce(t, group=self.group)
 
     def finish(self):
         self._flush()

@@ -74,17 +74,21 @@ class FusedAdamW(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             st = nat.stream_ptr(ps[0].device)
             hyper = group["hyper"]
+            # predicated on the device error word: no update while a validation error (flagged by
+            # this step's preamble / topology build, raised lazily) is pending — as the reference,
+            # whose exception comes before optimizer.step()
+            err = nat.error_word(ps[0].device).ptr()
             fp, fg = _flat_span(ps), _flat_span([p.grad for p in ps])
             fm, fv = group["flat_state"]
             if fp is not None and fg is not None:
                 nat.check(L.mgn_adamw_dev(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
-                                          nat.ptr(hyper), b1, b2, group["eps"], group["weight_decay"], st))
+                                          nat.ptr(hyper), b1, b2, group["eps"], group["weight_decay"], err, st))
             else:
                 for p in ps:
                     s = self.state[p]
                     nat.check(L.mgn_adamw_dev(nat.ptr(p), nat.ptr(p.grad.contiguous()), nat.ptr(s["exp_avg"]),
                                               nat.ptr(s["exp_avg_sq"]), p.numel(), nat.ptr(hyper), b1, b2,
-                                              group["eps"], group["weight_decay"], st))
+                                              group["eps"], group["weight_decay"], err, st))
 
     def _init_state(self, group, ps):
         n = sum(p.numel() for p in ps)

@@ -24,9 +24,20 @@ capture() warms the allocator and the library up with `warmup` eager steps and t
 piece of state they touched (parameters, optimizer moments and step count, scheduler, learning rate,
 normalizer buffers), so N calls are exactly N reference updates. The captured step owns one flat
 gradient buffer; the all-reduce and AdamW always read THAT buffer (re-pointing p.grad at it when
-eager() or zero_grad() moved it). Validation errors flagged on libmgn's device error word (node types
-outside the one-hot range) surface as the reference's RuntimeError at most one step late, without a
-host synchronisation per step.
+eager() or zero_grad() moved it).
+
+New batches: the loss mask (node types) and, data-parallel, the global masked-node count are taken
+from the CURRENT batch every step (the count rides in the statistics all-reduce). A captured step
+replays the tensors it recorded: assigning a new batch (`step.batch = b`) copies b's x / y /
+edge_attr into them when b shares the recorded edge_index (same tensor, unmodified); any other new
+batch is re-captured (a different topology).
+
+Validation errors flagged on libmgn's device error word (out-of-range edge_index, node types outside
+the one-hot range) surface as the reference's IndexError / RuntimeError at most one step late,
+without a host synchronisation per step. The device predicates the state updates on that word (ABI
+v11: no AdamW update, no node / edge normalizer accumulation while an error is pending), and the
+raise rewinds the host-side step count and LR schedule by the updates the device skipped, so a loop
+that catches the error and skips the batch continues from the state the reference would have.
 """
 import os
 
@@ -34,7 +45,7 @@ import torch
 import torch.distributed as dist
 
 from graphphysics import _native as nat
-from graphphysics.training.distributed import GradBuckets, allreduce_gradients, flat_grad_buffer, global_mask_count
+from graphphysics.training.distributed import GradBuckets, allreduce_gradients, flat_grad_buffer
 from graphphysics.utils.loss import masked_mse
 from graphphysics.utils.nodetype import NodeType
 
@@ -48,7 +59,6 @@ class TrainStep:
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         # data_parallel=True forces the exchanging step at any world size (tests run it on 1 rank)
         self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
-        self.node_type = batch.x[:, sim.node_type_index]
         self.params = [p for p in sim.parameters() if p.requires_grad]
         self.use_graph = graph
         self.graph = None
@@ -63,8 +73,14 @@ class TrainStep:
                 and dist.is_initialized():
             self.overlap = dist.get_backend(group) == "nccl"
         self.buckets = None
+        self._static = None  # graph mode: the batch tensors the graph was recorded on
         if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
+
+    @property
+    def node_type(self):
+        """Node types of the CURRENT batch (the loss mask)."""
+        return self.batch.x[:, self.sim.node_type_index]
 
     def _seed(self, loss):
         """d loss / d loss = 1 from a resident tensor (autograd would launch a fill kernel per step)."""
@@ -78,20 +94,55 @@ class TrainStep:
         return masked_mse(tdn, net, self.node_type, self.masks, count=self._count)
 
     def _prologue(self):
+        """Data parallel: this batch's normaliser statistics AND its masked-node count, summed over
+        ranks in one all-reduce (every step: the batch may have changed)."""
         if self.dp:
-            if self._count is None:
-                self._count = global_mask_count(self.node_type, self.masks, self.group)
-            self.sim.exchange_statistics(self.batch, self.group)
+            self._count = self.sim.exchange_statistics(self.batch, self.group, loss_masks=self.masks)
+
+    def _raised(self, ex):
+        """A validation error of an earlier step surfaced (reference IndexError / RuntimeError): the
+        device skipped every optimizer update since (mgn_adamw_dev predication), so rewind the
+        host-side counters by as many. Every poll point of a step comes before its own stage()."""
+        n = getattr(ex, "mgn_skipped_updates", 0)
+        if n:
+            self._rewind(n)
+
+    def _rewind(self, n):
+        for g in self.opt.param_groups:
+            if "step_count" in g:
+                g["step_count"] = max(g["step_count"] - n, 0)
+                for p in g["params"]:
+                    st = self.opt.state.get(p)
+                    if st is not None and "step" in st:
+                        st["step"] = torch.tensor(float(g["step_count"]))
+        sc = self.sched
+        sc.last_epoch -= n
+        if hasattr(sc, "get_lr_factor"):  # CosineWarmupScheduler: closed form
+            lrs = [b * sc.get_lr_factor(epoch=sc.last_epoch) for b in sc.base_lrs]
+        else:
+            import warnings
+
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                lrs = sc.get_lr()
+        for g, lr in zip(self.opt.param_groups, lrs):
+            g["lr"] = lr
+        sc._last_lr = list(lrs)
 
     def eager(self):
-        nat.poll_errors(self.batch.x.device)
-        self.opt.zero_grad(set_to_none=True)
-        self._prologue()
-        loss = self._loss()
+        try:
+            nat.poll_errors(self.batch.x.device)
+            self.opt.zero_grad(set_to_none=True)
+            self._prologue()
+            loss = self._loss()  # the Simulator / topology build poll the error word too
+        except (IndexError, RuntimeError) as ex:
+            self._raised(ex)
+            raise
         loss.backward(self._seed(loss))
         if self.dp:
             allreduce_gradients(self.params, self.group)
         self.opt.step()
+        nat.error_word(self.batch.x.device).arm()  # the copy-back carries the optimizer's skip count
         self.sched.step()
         return loss
 
@@ -128,7 +179,15 @@ class TrainStep:
 
     def capture(self, warmup=2, on_record=None):
         """Run `warmup` eager steps on a side stream (allocator + library state), restore the state
-        they changed (so they are not extra updates), then record one step."""
+        they changed (so they are not extra updates), then record one step. The graph reads private
+        copies of the batch's x / y / edge_attr (later batches are copied into them, never into the
+        caller's tensors) and the batch's edge_index itself (its topology is cached per tensor)."""
+        from graphphysics.utils.data import Data
+
+        b = self.batch
+        extra = {k: getattr(b, k) for k in ("pos",) if getattr(b, k, None) is not None}
+        self.batch = Data(x=b.x.clone(), y=b.y.clone(), edge_attr=b.edge_attr.clone(), edge_index=b.edge_index,
+                          **extra)
         snap = self._snapshot()
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
@@ -143,23 +202,36 @@ class TrainStep:
         if on_record is not None:
             on_record()
         self._prologue()  # pending statistics exist before recording (the graph reads their buffers)
-        try:
-            g, loss = self._record()
-        except Exception as ex:  # noqa: BLE001 — an RCCL stack that cannot record collectives
-            if not self.overlap:
-                raise
-            import warnings
-
-            warnings.warn("recording the overlapped gradient all-reduce failed (%s); the all-reduce runs "
-                          "after the replay instead" % ex)
-            self.overlap = False
-            self.opt.zero_grad(set_to_none=True)
-            self._prologue()
-            g, loss = self._record()
+        # no fallback: a failure to record the overlapped all-reduce raises on every rank (a rank that
+        # silently re-recorded without it would issue a different collective sequence)
+        g, loss = self._record()
         self.graph, self.static_loss = g, loss
         self._graph_grads = [p.grad for p in self.params]
         self._gflat = flat_grad_buffer(self.params)
+        b = self.batch
+        self._static = {"batch": b, "x": b.x, "y": b.y, "edge_attr": b.edge_attr, "edge_index": b.edge_index,
+                        "ei_version": b.edge_index._version}
         return self
+
+    def _sync_batch(self):
+        """Graph mode: the replay reads the tensors it was recorded on. A new batch sharing the
+        recorded edge_index is copied into them; any other new batch (or an edge_index modified in
+        place: the recorded topology would be stale) is re-captured."""
+        st = self._static
+        b = self.batch
+        if b is st["batch"] and all(getattr(b, k) is st[k] for k in ("x", "y", "edge_attr", "edge_index")) \
+                and b.edge_index._version == st["ei_version"]:
+            return
+        same = b.edge_index is st["edge_index"] and b.edge_index._version == st["ei_version"] and all(
+            getattr(b, k).shape == st[k].shape and getattr(b, k).dtype == st[k].dtype for k in ("x", "y", "edge_attr"))
+        if same:
+            with torch.no_grad():
+                for k in ("x", "y", "edge_attr"):
+                    if getattr(b, k) is not st[k]:
+                        st[k].copy_(getattr(b, k))
+            self.batch = st["batch"]
+        else:
+            self.graph = None  # re-captured on the new batch by __call__
 
     def _record(self):
         g = torch.cuda.CUDAGraph()
@@ -202,7 +274,13 @@ class TrainStep:
         if not self.use_graph:
             return self.eager()
         dev = self.batch.x.device
-        nat.poll_errors(dev)
+        try:
+            nat.poll_errors(dev)
+        except (IndexError, RuntimeError) as ex:
+            self._raised(ex)
+            raise
+        if self.graph is not None:
+            self._sync_batch()
         if self.graph is None:
             self.capture()
         self._bind_graph_grads()

@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 10
+#define MGN_ABI_VERSION 11
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -64,6 +64,17 @@ const char* mgn_last_error(void);
 #define MGN_ERR_EDGE_INDEX 1u /* edge_index outside [0, N): reference IndexError (ATen index)         */
 #define MGN_ERR_TYPE_NEG 2u   /* node type < 0 or NaN: F.one_hot "Class values must be non-negative." */
 #define MGN_ERR_TYPE_BIG 4u   /* node type >= n_types: "Class values must be smaller than num_classes." */
+#define MGN_ERR_ANY 0xFFFFu   /* any validation error (bits 0-15)                                      */
+/* State updates are predicated on the word, so an error raised lazily (one call late) leaves the
+ * training state as the reference's immediate exception would (ABI v11): mgn_adamw_dev skips its
+ * update while any MGN_ERR_ANY bit is set, counts the skip in bits 16-23 (MGN_ERR_SKIP_ONE each,
+ * saturating at 255) and sets MGN_ERR_STALE; mgn_simulator_preamble skips the node / edge
+ * normalizers' accumulation while any bit is set (the reference's F.one_hot raises after the output
+ * normalizer has accumulated, simulator.py:_build_input_graph) and the output normalizer's once
+ * MGN_ERR_STALE is set (the error belongs to an earlier step the reference would have stopped at). */
+#define MGN_ERR_SKIP_ONE (1u << 16)
+#define MGN_ERR_SKIP_MASK (0xFFu << 16)
+#define MGN_ERR_STALE (1u << 31)
 
 /* ---------------------------------------------------------------- topology */
 typedef struct mgn_topology {
@@ -342,10 +353,11 @@ int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
               int64_t step, mgn_stream_t stream);
 
 /* As mgn_adamw with lr and step read from device memory: hyper = double[2] {lr, step}. The launch
- * can be captured in a hipGraph and replayed with a new schedule (host updates hyper). */
+ * can be captured in a hipGraph and replayed with a new schedule (host updates hyper). err_word
+ * (nullable, ABI v11): no update while a validation error is pending on it (see MGN_ERR_STALE). */
 int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
-                  mgn_stream_t stream);
+                  uint32_t* err_word, mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- graph construction */
 /* On-device replacements for the reference's per-sample host preprocessing (SURVEY.md §8(f)

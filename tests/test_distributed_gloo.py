@@ -98,6 +98,83 @@ def test_two_rank_step_equals_single_process_step(prologue):
         torch.testing.assert_close(g0, p.grad, rtol=2e-4, atol=1e-6)
 
 
+def _ddp_worker(rank, world, port, out, hook):
+    """The INTEGRATION.md recipe: DistributedDataParallel (the Lightning "ddp" strategy's wrapper)
+    with the SUM communication hook, global statistics and the global masked mean."""
+    import sys
+
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "graph-physics_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.distributed import global_masked_mse, sum_allreduce_hook
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+    from graphphysics.utils.nodetype import NodeType
+
+    torch.set_num_threads(1)
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    sim.set_process_group(dist.group.WORLD)
+    ddp = DDP(sim)
+    if hook:
+        ddp.register_comm_hook(None, sum_allreduce_hook)
+    d = _shard(b, rank, world)
+    data = Data(**{k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in d.items()})
+    net, tdn, _ = ddp(data)
+    loss = global_masked_mse(tdn, net, data.x[:, 2], [NodeType.NORMAL, NodeType.OUTFLOW], dist.group.WORLD)
+    loss.backward()
+    torch.save({"grads": [p.grad.clone() for p in sim.parameters()]}, os.path.join(out, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hook", [True, False])
+def test_ddp_recipe_with_sum_hook_equals_single_process(hook):
+    """INTEGRATION.md's multi-GPU recipe on CPU (gloo, 2 ranks): DDP + sum_allreduce_hook +
+    global_masked_mse reproduces the single-process gradients on the union batch; DDP's default
+    averaging hook would give exactly 1/world_size of them (shown by the hook=False case)."""
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+
+    port = 29900 + os.getpid() % 1000 + int(hook)
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_ddp_worker, args=(2, port, out, hook), nprocs=2, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(2)]
+    b = meshes.cylinder_batch(4, jitter=0.01)
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    _step(sim, {k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}, None)
+    scale = 1.0 if hook else 0.5
+    for g0, g1, p in zip(r[0]["grads"], r[1]["grads"], sim.parameters()):
+        assert torch.equal(g0, g1)
+        torch.testing.assert_close(g0, scale * p.grad, rtol=2e-4, atol=1e-6)
+
+
+def test_statistics_exchange_carries_each_batchs_mask_count():
+    """exchange_statistics(loss_masks=...) returns the masked-node count of the CURRENT batch (one
+    process: the local count; the data-parallel step calls it every step), at a stable address."""
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    seen, ptrs = [], set()
+    for k, frac in enumerate((0.0, 0.1, 0.3)):
+        b = meshes.cylinder_batch(2, t=k)
+        x = b["x"].copy()
+        rng = np.random.default_rng(k)
+        x[(x[:, 2] == 0) & (rng.random(x.shape[0]) < frac), 2] = 6
+        data = Data(x=torch.from_numpy(x), y=torch.from_numpy(b["y"]), edge_index=torch.from_numpy(b["edge_index"]),
+                    edge_attr=torch.from_numpy(b["edge_attr"]))
+        c = sim.exchange_statistics(data, None, loss_masks=[0, 5])
+        seen.append((float(c[0]), int(np.isin(x[:, 2], (0, 5)).sum())))
+        ptrs.add(c.data_ptr())
+    assert all(a == e for a, e in seen) and len({e for _, e in seen}) == 3, seen
+    assert len(ptrs) == 1
+
+
 def test_flat_grad_buffer_detection():
     from graphphysics.training.distributed import flat_grad_buffer
 

@@ -259,6 +259,45 @@ def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
         assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
 
 
+@pytest.mark.parametrize("n,e", [(1100, 1000), (3000, 700)])
+def test_epd_bf16_h128_more_nodes_than_edges(n, e):
+    """bf16 h=128 (chained kernels + weight-gradient ring) on graphs with more nodes than edges: the
+    ring's W0-projection jobs run over node rows into the edge MLP's slab buffer, which is sized for
+    the edge row count — their chunk count must stay within it (N=1100, E=1000 gives 18 node chunks
+    against 16 edge slabs). Bound: as test_epd_cylinder_vs_oracle's bf16 case (2 × PyTorch's bf16
+    autocast of the reference, both vs fp64)."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    g = torch.Generator().manual_seed(11)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(e, 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    mp, h = 2, 128
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    rp = dict(ref.named_parameters())
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(x.double(), ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = O.encode_process_decode(x, ei, ea, pac, mp)
+    (yac.float() * gy).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=torch.bfloat16).to(DEV)
+    for _ in range(2):  # twice: the second backward reuses the cached topology / workspaces
+        m.zero_grad(set_to_none=True)
+        y = m(Data(x=x.to(DEV), edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+        (y * gy.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert relerr(y, y64) <= 2 * relerr(yac, y64)
+    for k, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all(), k
+        assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
+
+
 # ----------------------------------------------------------------------------- optimiser / primitives
 def test_adamw_matches_torch():
     from graphphysics.training.optim import FusedAdamW
