@@ -44,8 +44,13 @@ def parse():
     ap.add_argument("--mp", type=int, default=15)
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-steps", type=int, default=10,
-                    help="timed CPU baseline steps after 3 warm-up steps (SURVEY §8d; 0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=3,
+                    help="timed CPU baseline steps after one warm-up step: a bounded sample (~30 s on 16 cores) "
+                         "of the same workload, median reported (0: skip)")
+    ap.add_argument("--sustain", type=float, default=5.0,
+                    help="seconds of further replayed steps after the timed K (reported as `sustained`)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the Config B fp32 and Config A rows (N=1 only)")
     ap.add_argument("--no-mse", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
@@ -143,6 +148,156 @@ def scatter_bytes(n, e, h, es):
     return e * h * es + n * h * es + 4 * e + 4 * (n + 1)
 
 
+def build_step(a, dev, rank, mesh, world):
+    """Workload + Simulator + FusedAdamW + schedule + TrainStep of configuration `a`."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.models.simulator import Simulator
+    from graphphysics.training.optim import FusedAdamW
+    from graphphysics.training.step import TrainStep
+    from graphphysics.utils.scheduler import CosineWarmupScheduler
+
+    cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    b, data, lay, workload, datadesc = make_workload(a, dev, rank, mesh)
+    torch.manual_seed(0)
+    model = EncodeProcessDecode(a.mp, lay["node_in"], lay["edge_in"], lay["out"], a.hidden, compute_dtype=cdt)
+    sim = Simulator(lay["node_in"], lay["edge_in"], lay["out"], lay["fs"][0], lay["fs"][1], lay["os"][0],
+                    lay["os"][1], lay["nti"], model, dev)
+    opt = FusedAdamW(list(sim.parameters()), lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
+    sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
+    sim.train()
+    step = TrainStep(sim, opt, sched, data, graph=not a.no_graph, data_parallel=(world > 1 or a.dp))
+    return step, sim, b, data, lay, workload, datadesc
+
+
+def warm(a, step):
+    if step.use_graph:
+        step.capture(warmup=max(a.warmup - 1, 1))
+        step()  # first replay
+    else:
+        for _ in range(a.warmup):
+            step()
+    torch.cuda.synchronize()
+
+
+def profile_classes(a, step):
+    """Per-kernel-class durations: HIP events on the launch stream around every kernel of K steps run
+    eagerly (the same kernels, shapes and launch order the replayed graph contains), after two
+    unprofiled eager steps (the first eager step after replays pays one-time costs)."""
+    from graphphysics import _native as nat
+
+    for _ in range(2):
+        step.eager()
+    torch.cuda.synchronize()
+    nat.profile_enable(True)
+    for _ in range(a.steps):
+        step.eager()
+    torch.cuda.synchronize()
+    prof = nat.profile_collect()
+    nat.profile_enable(False)
+    return prof
+
+
+def analyse(a, prof, sim, lay, N, E, dt):
+    """Per-class work rates and the roofline of the dominant class."""
+    h = a.hidden
+    es = 2 if a.dtype == "bf16" else 4
+    nparams = sum(p.numel() for p in sim.parameters())
+    nweights = sum(m.weight.numel() for m in sim.model.modules() if isinstance(m, torch.nn.Linear))
+    work = class_work(N, E, h, a.mp, lay, nparams, nweights, es)
+    kinds = {}
+    for k, (ms, cnt) in prof.items():
+        if cnt:
+            kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2),
+                        "ms_per_step": round(ms / a.steps, 4)}
+            if k in work:
+                bound, amount = work[k]
+                per_s = amount * a.steps / (ms / 1000)
+                if bound == "mfma":
+                    kinds[k].update(bound="mfma", tflops=round(per_s / 1e12, 2),
+                                    frac=round(per_s / 1e12 / PEAK[a.dtype], 4))
+                else:
+                    kinds[k].update(bound="hbm", gbs=round(per_s / 1e9, 1), frac=round(per_s / 1e9 / HBM_PEAK, 4))
+    roof = None
+    wl = workload_key(a)
+    step_flops = 3 * (a.mp * (12 * h * h * E + 10 * h * h * N) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
+                      + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
+    step_tf = step_flops * a.steps / dt / 1e12
+    if kinds:
+        # dominant kernel class = largest device time per step in the REPLAYED graph (rocprofv3 kernel
+        # trace of this bench command on these sources, recorded with the PMC passes under profiles/);
+        # without such a record, the largest class of the eager HIP-event profile
+        rep = replay_lookup(wl)
+        cands = [k for k in rep.get("replay", {}) if k in kinds]
+        if cands:
+            dom = max(cands, key=lambda k: rep["replay"][k]["us_per_step"])
+            picked = "replay: %s (%s)" % (rep["source"], ", ".join(
+                "%s %.1f us/step" % (k, rep["replay"][k]["us_per_step"])
+                for k in sorted(cands, key=lambda k: -rep["replay"][k]["us_per_step"])[:3]))
+        else:
+            dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
+            picked = "eager HIP-event profile (no replay trace recorded for these sources and workload)"
+        kd = kinds[dom]
+        bound, amount = work.get(dom, ("mfma", 0))
+        per_launch = amount * a.steps / kd["launches"]
+        avg_s = kd["total_ms"] / 1000 / kd["launches"]
+        ach = per_launch / avg_s / (1e12 if bound == "mfma" else 1e9)
+        peak = PEAK[a.dtype] if bound == "mfma" else HBM_PEAK
+        pmc = pmc_lookup(dom, wl)
+        roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak,
+                "unit": "TFLOP/s" if bound == "mfma" else "GB/s", "frac": round(ach / peak, 4),
+                "traffic": pmc.get("hbm_bytes"), "traffic_source": pmc.get("source"),
+                "mfma_util_measured": pmc.get("mfma_util"), "dominant_from": picked,
+                ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per_launch,
+                "avg_launch_us": round(avg_s * 1e6, 2), "launches_per_step": kd["launches"] / a.steps,
+                "peak_source": "MI355X_MICROARCH.md: dense bf16 MFMA 2.5 PFLOP/s (fp32 MFMA 157.3), HBM3E 8 TB/s",
+                "step": {"tflops_per_s": round(step_tf, 2), "frac": round(step_tf / PEAK[a.dtype], 4),
+                         "flops_per_step": step_flops, "note": "3 x F_fwd (SURVEY §8d) / measured ms_per_step"}}
+        if "fwd_node" in kinds:  # the segmented sum is fused into the node-MLP forward (CSC segments)
+            sb = scatter_bytes(N, E, h, es)
+            t = kinds["fwd_node"]["total_ms"] / 1000 / kinds["fwd_node"]["launches"]
+            roof["scatter"] = {"kernel": "fwd_node (segment sum fused into the node-MLP forward)",
+                               "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
+                               "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
+        if "combine" in kinds:
+            sb = 2 * scatter_bytes(N, E, h, es)
+            t = kinds["combine"]["total_ms"] / 1000 / kinds["combine"]["launches"]
+            roof["gather_bwd"] = {"kernel": "combine (dP_i / dP_j segment sums over both index directions)",
+                                  "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
+                                  "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
+    return kinds, roof
+
+
+def secondary(a0, dev, mesh, label, cpu_steps=0, **over):
+    """One more single-GPU configuration timed inside the same invocation (BASELINE.md Config A / B
+    rows): warm-up, K timed replayed steps, the eager per-class profile and its roofline, optionally
+    the CPU baseline of the same configuration."""
+    a = argparse.Namespace(**vars(a0))
+    for k, v in over.items():
+        setattr(a, k, v)
+    step, sim, b, data, lay, workload, datadesc = build_step(a, dev, 0, mesh, 1)
+    N, E = data.x.shape[0], data.edge_index.shape[1]
+    warm(a, step)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kinds, roof = analyse(a, profile_classes(a, step) if not a.no_profile else {}, sim, lay, N, E, dt)
+    r = {"label": label, "workload": workload, "dtype": a.dtype, "mp": a.mp, "hidden": a.hidden,
+         "graphs": a.batch, "nodes": N, "edges": E, "steps": a.steps, "value": round(a.steps / dt, 3),
+         "unit": "steps/s", "ms_per_step": round(1000 * dt / a.steps, 3),
+         "execution": "hipGraph replay of the whole step" if step.use_graph else "eager", "roofline": roof,
+         "kernels": {k: {f: v[f] for f in ("avg_us", "ms_per_step", "frac") if f in v} for k, v in kinds.items()}}
+    if cpu_steps:
+        a.cpu_steps = cpu_steps
+        r["cpu_baseline"] = cpu_baseline(a, b, lay, warmup=3)
+        r["speedup_vs_cpu"] = round(r["value"] / r["cpu_baseline"]["value"], 1)
+    del step, sim, data
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return r
+
+
 def main():
     a = parse()
     if a.print_workload:
@@ -175,36 +330,13 @@ def main():
         dist.barrier()
     ge._paths()
     from graphphysics import _native as nat
-    from graphphysics.models.processors import EncodeProcessDecode
-    from graphphysics.models.simulator import Simulator
-    from graphphysics.training.optim import FusedAdamW
-    from graphphysics.training.step import TrainStep
     from graphphysics.utils import meshes
-    from graphphysics.utils.data import Data
-    from graphphysics.utils.nodetype import NodeType
-    from graphphysics.utils.scheduler import CosineWarmupScheduler
 
     nat.load()
-    cdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     mesh = meshes.load_cylinder_mesh()
-    b, data, lay, workload, datadesc = make_workload(a, dev, rank, mesh)
+    step, sim, b, data, lay, workload, datadesc = build_step(a, dev, rank, mesh, world)
     N, E = data.x.shape[0], data.edge_index.shape[1]
-    torch.manual_seed(0)
-    model = EncodeProcessDecode(a.mp, lay["node_in"], lay["edge_in"], lay["out"], a.hidden, compute_dtype=cdt)
-    sim = Simulator(lay["node_in"], lay["edge_in"], lay["out"], lay["fs"][0], lay["fs"][1], lay["os"][0],
-                    lay["os"][1], lay["nti"], model, dev)
-    params = list(sim.parameters())
-    opt = FusedAdamW(params, lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
-    sched = CosineWarmupScheduler(opt, warmup=1000, max_iters=10 ** 6)
-    sim.train()
-    step = TrainStep(sim, opt, sched, data, graph=not a.no_graph, data_parallel=(world > 1 or a.dp))
-    if step.use_graph:
-        step.capture(warmup=max(a.warmup - 1, 1))
-        step()  # first replay
-    else:
-        for _ in range(a.warmup):
-            step()
-    torch.cuda.synchronize()
+    warm(a, step)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -224,20 +356,24 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    prof = {}
-    if not a.no_profile:
-        # Per-kernel durations: HIP events on the launch stream around every kernel of K more steps
-        # run eagerly (the same kernels, shapes and launch order the replayed graph contains), after
-        # two unprofiled eager steps (the first eager step after the replays pays one-time costs).
-        for _ in range(2):
-            step.eager()
+    # sustained rate: the same step replayed for about `sustain` more seconds (reported beside the
+    # headline, never as `value`; it also keeps the GPU visibly busy for the driver's sampler)
+    sus = None
+    if a.sustain > 0 and not a.fresh_batch:
+        n_s = max(int(a.sustain / max(dt / a.steps, 1e-4)), a.steps)
+        if world > 1:  # every rank replays the same count (collectives inside the step)
+            t = torch.tensor([n_s], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            n_s = int(t.item())
+        t1 = time.perf_counter()
+        for _ in range(n_s):
+            step()
         torch.cuda.synchronize()
-        nat.profile_enable(True)
-        for _ in range(a.steps):
-            step.eager()
-        torch.cuda.synchronize()
-        prof = nat.profile_collect()
-        nat.profile_enable(False)
+        if world > 1:
+            dist.barrier()
+        ds = time.perf_counter() - t1
+        sus = {"steps": n_s, "seconds": round(ds, 3), "value": round(world * n_s / ds, 3), "unit": "steps/s"}
+    prof = profile_classes(a, step) if not a.no_profile else {}
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -250,60 +386,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    h = a.hidden
-    es = 2 if a.dtype == "bf16" else 4
-    nparams = sum(p.numel() for p in sim.parameters())
-    nweights = sum(m.weight.numel() for m in sim.model.modules() if isinstance(m, torch.nn.Linear))
-    work = class_work(N, E, h, a.mp, lay, nparams, nweights, es)
-    kinds = {}
-    for k, (ms, cnt) in prof.items():
-        if cnt:
-            kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2),
-                        "ms_per_step": round(ms / a.steps, 4)}
-            if k in work:
-                bound, amount = work[k]
-                per_s = amount * a.steps / (ms / 1000)
-                if bound == "mfma":
-                    kinds[k].update(bound="mfma", tflops=round(per_s / 1e12, 2),
-                                    frac=round(per_s / 1e12 / PEAK[a.dtype], 4))
-                else:
-                    kinds[k].update(bound="hbm", gbs=round(per_s / 1e9, 1), frac=round(per_s / 1e9 / HBM_PEAK, 4))
-    roof = None
-    wl = workload_key(a)
-    step_flops = 3 * (a.mp * (12 * h * h * E + 10 * h * h * N) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
-                      + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
-    step_tf = step_flops * a.steps / dt / 1e12
-    if kinds:
-        # dominant kernel class = largest total time over ALL classes (rocprofv3 agrees: profiles/)
-        dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
-        kd = kinds[dom]
-        bound, amount = work.get(dom, ("mfma", 0))
-        per_launch = amount * a.steps / kd["launches"]
-        avg_s = kd["total_ms"] / 1000 / kd["launches"]
-        ach = per_launch / avg_s / (1e12 if bound == "mfma" else 1e9)
-        peak = PEAK[a.dtype] if bound == "mfma" else HBM_PEAK
-        pmc = pmc_lookup(dom, wl)
-        roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak,
-                "unit": "TFLOP/s" if bound == "mfma" else "GB/s", "frac": round(ach / peak, 4),
-                "traffic": pmc.get("hbm_bytes"), "traffic_source": pmc.get("source"),
-                "mfma_util_measured": pmc.get("mfma_util"),
-                ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per_launch,
-                "avg_launch_us": round(avg_s * 1e6, 2), "launches_per_step": kd["launches"] / a.steps,
-                "peak_source": "MI355X_MICROARCH.md: dense bf16 MFMA 2.5 PFLOP/s (fp32 MFMA 157.3), HBM3E 8 TB/s",
-                "step": {"tflops_per_s": round(step_tf, 2), "frac": round(step_tf / PEAK[a.dtype], 4),
-                         "flops_per_step": step_flops, "note": "3 x F_fwd (SURVEY §8d) / measured ms_per_step"}}
-        if "fwd_node" in kinds:  # the segmented sum is fused into the node-MLP forward (CSC segments)
-            sb = scatter_bytes(N, E, h, es)
-            t = kinds["fwd_node"]["total_ms"] / 1000 / kinds["fwd_node"]["launches"]
-            roof["scatter"] = {"kernel": "fwd_node (segment sum fused into the node-MLP forward)",
-                               "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
-                               "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
-        if "combine" in kinds:
-            sb = 2 * scatter_bytes(N, E, h, es)
-            t = kinds["combine"]["total_ms"] / 1000 / kinds["combine"]["launches"]
-            roof["gather_bwd"] = {"kernel": "combine (dP_i / dP_j segment sums over both index directions)",
-                                  "bytes_per_launch": sb, "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK,
-                                  "unit": "GB/s", "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
+    kinds, roof = analyse(a, prof, sim, lay, N, E, dt)
     value = world * a.steps / dt
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
@@ -312,8 +395,9 @@ def main():
         "data": "synthetic: %s, random-init weights (seed 0)" % datadesc,
         "execution": ("eager, a new batch (fresh x / y / edge_index / edge_attr tensors, topology rebuilt) "
                       "every step" if a.fresh_batch else "eager" if not step.use_graph else
-                      ("statistics all-reduce, then hipGraph replay of forward+loss+backward with the bucketed "
-                       "gradient all-reduce overlapped on a communication stream + AdamW" if step.overlap else
+                      ("statistics + mask-count all-reduce, then hipGraph replay of forward+loss+backward with "
+                       "the bucketed gradient all-reduce overlapped on a communication stream + AdamW"
+                       if step.overlap else
                        "hipGraph replay of forward+loss+backward; eager statistics/gradient all-reduce + AdamW")
                       if step.dp else "hipGraph replay of the whole step"),
         "config": {"workload": workload, "nodes_per_gpu": N, "edges_per_gpu": E,
@@ -322,6 +406,8 @@ def main():
                    "graphs_per_sec": round(value * (a.batch if a.workload == "cylinder" else 1), 2)},
         "roofline": roof, "kernels": kinds, "last_loss": last_loss,
     }
+    if sus is not None:
+        out["sustained"] = sus
 
     if not a.no_mse and a.workload == "cylinder":
         out["one_step_mse"] = one_step_mse(sim, mesh, dev, a)
@@ -329,11 +415,39 @@ def main():
         out["cpu_baseline"] = cpu_baseline(a, b, lay)
         if out["cpu_baseline"]:
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+    if world == 1 and not a.no_secondary and a.workload == "cylinder":
+        # BASELINE.md Config B in the reference's fp32 and Config A (training_config/cylinder.json
+        # as written: MP=5, h=32, fp32, one graph) with its CPU baseline, same invocation
+        del step, sim
+        torch.cuda.empty_cache()
+        sec = {}
+        if not (a.dtype == "fp32" and a.mp == 15 and a.hidden == 128 and a.batch == 8):
+            sec["cfgB_fp32"] = secondary(a, dev, mesh, "Config B in fp32 (the reference's dtype)", dtype="fp32",
+                                         mp=15, hidden=128, batch=8)
+        sec["cfgA"] = secondary(a, dev, mesh, "Config A: training_config/cylinder.json (MP=5, h=32, fp32, B=1)",
+                                cpu_steps=(20 if a.cpu_steps > 0 else 0), dtype="fp32", mp=5, hidden=32, batch=1)
+        out["secondary"] = sec
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def replay_lookup(workload):
+    """Per-class device time of the replayed step from the newest committed profiles/*_traffic.json
+    recorded on the same kernel sources (sha256 stamp) and workload (tools/pmc_traffic.py `replay`)."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import sources_sha
+
+    sha = sources_sha()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("sources_sha") == sha and d.get("workload") == workload and d.get("replay"):
+            return {"source": os.path.relpath(f, ROOT), "replay": d["replay"]}
+    return {}
 
 
 def pmc_lookup(kernel_class, workload):
@@ -398,9 +512,10 @@ def one_step_mse(sim, mesh, dev, a):
             "frames": "3->4, 4->5 (held out), B=1, weights after the timed steps"}
 
 
-def cpu_baseline(a, b, lay):
+def cpu_baseline(a, b, lay, warmup=1):
     """The reference algorithm on the host (oracle = op-for-op restatement of the reference's
-    PyTorch CPU path, pinned to golden vectors), same workload (Cfg B batch 8), fp32, all cores."""
+    PyTorch CPU path, pinned to golden vectors), same workload, fp32, all cores: `warmup` untimed
+    steps, then a.cpu_steps timed ones, median."""
     from oracle import mgn_oracle as O
 
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
@@ -420,7 +535,7 @@ def cpu_baseline(a, b, lay):
         O.l2_loss(tdn, net, x[:, lay["nti"]]).backward()
         opt.step()
 
-    for _ in range(3):  # warm-up (3 warm-up, >= 10 timed, median)
+    for _ in range(warmup):
         step()
     ts = []
     for _ in range(a.cpu_steps):
@@ -440,8 +555,9 @@ def cpu_baseline(a, b, lay):
     except OSError:
         pass
     return {"value": round(1.0 / med, 4), "unit": "steps/s", "cores": cores, "kind": "port",
-            "sample": "%d timed + 3 warm-up full steps of the same workload (N=%d, E=%d), torch %s fp32, median"
-                      % (a.cpu_steps, b["x"].shape[0], b["edge_index"].shape[1], torch.__version__),
+            "sample": "%d timed + %d warm-up full training steps of the same workload (MP=%d, h=%d, N=%d, E=%d), "
+                      "torch %s fp32, median" % (a.cpu_steps, warmup, a.mp, a.hidden, b["x"].shape[0],
+                                                 b["edge_index"].shape[1], torch.__version__),
             "cpu": model, "host": platform.node()}
 
 

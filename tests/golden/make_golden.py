@@ -367,6 +367,56 @@ def gen_trained_threads1():
     np.savez_compressed(os.path.join(HERE, "cylinder_trained_threads1.npz"), **out)
 
 
+def _train_reference(threads):
+    """The gen_trained run with `threads` intra-op threads; returns (sim, losses, held-out MSEs)."""
+    torch.set_num_threads(threads)
+    pos, tri, vel = load_cylinder()
+    n = pos.shape[0]
+    ei = face_to_edge_undirected(tri, n)
+    nt = node_types(pos, vel[0])
+    ea = edge_features(pos, ei)
+    datas = [frame_data(pos, ei, ea, nt, vel, t) for t in range(5)]
+    scratch = {}
+    sim = make_sim(15, 128)
+    train_steps(sim, [datas[i % 3] for i in range(TRAIN_STEPS)], scratch, "trained", lr=TRAIN_LR,
+                warmup=TRAIN_WARMUP, max_iters=TRAIN_STEPS)
+    ev = {}
+    eval_one_step(sim, datas[3:5], ev, "trained_eval")
+    return sim, scratch["trained/losses"], ev["trained_eval/one_step_mse"], ev["trained_eval/pred0"]
+
+
+def gen_trained_weights():
+    """The reference's OWN trained model in full: gen_trained's 8-thread run
+    (MP=15, h=128, 300 steps), its complete state_dict (fp32) and normaliser buffers, and its
+    held-out one-step MSE / prediction — so the build evaluates the very weights the reference
+    trained. Also the same run at 1, 2 and 4 threads: the reference's own run-to-run spread (its
+    CPU kernels sum in thread-count-dependent order; training is chaotic), from which the
+    train-from-init comparison takes its band."""
+    ref = np.load(os.path.join(HERE, "cylinder_trained.npz"))
+    out = {"train_steps": np.array(TRAIN_STEPS)}
+    sim, losses, mse, pred0 = _train_reference(8)
+    # the same run as the committed gen_trained fixture (same machine image, same thread count)
+    out["matches_cylinder_trained"] = np.array(bool(np.array_equal(losses, ref["trained/losses"])))
+    out["losses"] = losses
+    out["one_step_mse"] = mse
+    out["pred0"] = pred0
+    for k, v in sim.state_dict().items():
+        out["sd::" + k] = v.detach().cpu().numpy().copy()
+    for name in ["_output_normalizer", "_node_normalizer", "_edge_normalizer"]:
+        nrm = getattr(sim, name)
+        for b in ("_acc_sum", "_acc_sum_squared", "_acc_count", "_num_accumulations"):
+            out[f"norm::{name}::{b}"] = getattr(nrm, b).detach().cpu().numpy().copy()
+    runs = {8: (losses, mse)}
+    for th in (1, 2, 4):
+        _, l_t, m_t, _ = _train_reference(th)
+        runs[th] = (l_t, m_t)
+    out["chaos_threads"] = np.array(sorted(runs))
+    out["chaos_losses"] = np.stack([runs[t][0] for t in sorted(runs)])
+    out["chaos_one_step_mse"] = np.stack([runs[t][1] for t in sorted(runs)])
+    torch.set_num_threads(8)
+    np.savez_compressed(os.path.join(HERE, "cylinder_trained_weights.npz"), **out)
+
+
 # ----------------------------------------------------------------------------- validation rollout
 def _reference_lightning_module():
     """The reference LightningModule class (lightning_module.py) importable without lightning and

@@ -63,7 +63,24 @@ def load(path):
     return per
 
 
-def main(workload, out, fetch_csv, write_csv, sq_csv=None):
+def replay_classes(trace_csv, steps):
+    """Per-class device time of the last `steps` REPLAYED steps of a rocprofv3 kernel trace (a step
+    starts at its preamble_stats launch, as tools/gap_summary.py): {class: {us_per_step, launches_per_step,
+    avg_us}} — what bench.py picks its dominant kernel class from (the replay, not eager steps)."""
+    rows = sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("preamble_stats")]
+    seg = rows[starts[-steps]:]
+    agg = {}
+    for r in seg:
+        c = kernel_class(r["Kernel_Name"])
+        if c is None:
+            continue
+        agg.setdefault(c, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {c: {"us_per_step": round(sum(v) / steps, 2), "launches_per_step": len(v) / steps,
+                "avg_us": round(sum(v) / len(v), 2)} for c, v in agg.items()}
+
+
+def main(workload, out, fetch_csv, write_csv, sq_csv=None, trace_csv=None, steps=5):
     f, w, q = load(fetch_csv), load(write_csv), load(sq_csv)
     res = {}
     for key in sorted(set(f) | set(w) | set(q)):
@@ -81,8 +98,12 @@ def main(workload, out, fetch_csv, write_csv, sq_csv=None):
         if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("GRBM_GUI_ACTIVE"):
             d["mfma_util"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * d["GRBM_GUI_ACTIVE"] / XCDS)
         res[key] = d
-    json.dump({"sources_sha": sources_sha(), "workload": workload, "fetch_correction": 2.0,
-               "unit": "per launch (median over launches)", "kernels": res}, open(out, "w"), indent=1)
+    doc = {"sources_sha": sources_sha(), "workload": workload, "fetch_correction": 2.0,
+           "unit": "per launch (median over launches)", "kernels": res}
+    if trace_csv:
+        doc["replay"] = replay_classes(trace_csv, int(steps))
+        doc["replay_source"] = "rocprofv3 --kernel-trace of the same bench command, last %s replayed steps" % steps
+    json.dump(doc, open(out, "w"), indent=1)
     for k, d in res.items():
         print(f"{d['class']:12s} {d.get('hbm_bytes', 0) / 1e6:8.1f} MB  mfma_util {d.get('mfma_util', float('nan')):.3f}"
               f"  {d['kernel'][:60]} grid={d['grid']}")
