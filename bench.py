@@ -204,6 +204,10 @@ def analyse(a, prof, sim, lay, N, E, dt):
     nparams = sum(p.numel() for p in sim.parameters())
     nweights = sum(m.weight.numel() for m in sim.model.modules() if isinstance(m, torch.nn.Linear))
     work = class_work(N, E, h, a.mp, lay, nparams, nweights, es)
+    if not prof.get("wgrad", (0, 0))[1] and prof.get("wgrad_dense", (0, 0))[1]:
+        # no ring launches (fp32, or h != 128): every weight gradient, the processor blocks' too,
+        # runs on the generic kernel the profiler files under wgrad_dense
+        work["wgrad_dense"] = ("mfma", work["wgrad_dense"][1] + work["wgrad"][1])
     kinds = {}
     for k, (ms, cnt) in prof.items():
         if cnt:

@@ -21,7 +21,8 @@
 
 // Diagnostics builds only (-DMGN_ABLATE=bits, results wrong when nonzero; see mgn_mlp.hip): edge
 // forward 1 = P gathers from row 0 (cache-resident), 2 = no P loads, 4 = no weight-staging loads,
-// 8 = no stores of outputs / saves; node forward 16 = no aggregation gathers
+// 8 = no stores of outputs / saves; node forward 16 = no aggregation gathers; node kernels 32 = every
+// global weight fragment read from fragment 0 (L1-hot: the cost of streaming them from L2)
 #ifndef MGN_ABLATE
 #define MGN_ABLATE 0
 #endif
@@ -758,7 +759,7 @@ __device__ __forceinline__ int gfrag_voff(int lane) {
     return (r * 8 + 4 * (g & 1) + 16 * (g >> 1) * 8) * 2;  // bytes
 }
 __device__ __forceinline__ bf16x8 gfrag(__amdgpu_buffer_rsrc_t rs, int voff, int tile) {
-    const int so = tile * 64 * 8 * 2;  // bytes
+    const int so = (MGN_ABLATE & 32) ? 0 : tile * 64 * 8 * 2;  // bytes (ablation 32: one L1-hot fragment)
     const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so, 0));
     const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so + 2 * 16 * 8 * 2, 0));
     const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};

@@ -499,9 +499,8 @@ class EPDFunction(torch.autograd.Function):
                         pend_b = b
                         pend_hi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
                     if (pend_hi - boff[2 * b]) * 4 >= GRAD_GROUP_BYTES or b == 0:
-                        # blocks b..pend_b: consecutive descriptors from reds[2b]
-                        nat.check(L.mgn_wgrad_reduce_many(ctypes.byref(reds, 2 * b * ctypes.sizeof(nat.WgradReduce)),
-                                                          2 * (pend_b - b + 1), st))
+                        # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
+                        nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1), st))
                         _grad_ready(G, boff[2 * b], pend_hi)
                         pend_hi = pend_b = None
             elif not overlap:

@@ -287,11 +287,12 @@ def _aten_eval(ref, x, ei, ea, gy, mp, dtype, autocast=False):
             y = _epd_ckpt(xd, ei, ed, p, mp)
     else:
         y = _epd_ckpt(xd, ei, ed, p, mp)
-    (y.to(gy.dtype) * gy).sum().backward()
+    keys = list(p)
+    grads = torch.autograd.grad((y.to(gy.dtype) * gy).sum(), [xd, ed] + [p[k] for k in keys])
     torch.cuda.synchronize()
-    out = {"y": y.detach().double().cpu(), "x": xd.grad.double().cpu(), "e": ed.grad.double().cpu()}
-    out.update({k: v.grad.double().cpu() for k, v in p.items()})
-    del p, xd, ed, y
+    out = {"y": y.detach().double().cpu(), "x": grads[0].double().cpu(), "e": grads[1].double().cpu()}
+    out.update({k: g.double().cpu() for k, g in zip(keys, grads[2:])})
+    del p, xd, ed, y, grads
     torch.cuda.empty_cache()
     return out
 

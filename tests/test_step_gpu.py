@@ -117,14 +117,23 @@ def _train(graph, dtype=torch.bfloat16):
     return sim, opt, sch, st
 
 
+def _norm(n):
+    return {k: b.detach().clone() for k, b in n.named_buffers()}
+
+
 def _state(sim, opt, sch):
     g = opt.param_groups[0]
     return {"params": [p.detach().clone() for p in sim.parameters()],
             "moments": [t.clone() for t in g["flat_state"]],
-            "out_norm": [b.clone() for b in sim._output_normalizer.buffers()],
-            "node_norm": [b.clone() for b in sim._node_normalizer.buffers()],
-            "edge_norm": [b.clone() for b in sim._edge_normalizer.buffers()],
+            "out_norm": _norm(sim._output_normalizer), "node_norm": _norm(sim._node_normalizer),
+            "edge_norm": _norm(sim._edge_normalizer),
             "step_count": g["step_count"], "lr": g["lr"], "last_epoch": sch.last_epoch}
+
+
+def _same(a, b):
+    if isinstance(a, dict):
+        return all(torch.equal(a[k], b[k]) for k in a)
+    return all(torch.equal(x, y) for x, y in zip(a, b))
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -152,16 +161,16 @@ def test_bad_node_type_step_leaves_state_like_reference(graph, bad):
             torch.cuda.synchronize()
     after = _state(sim, opt, sch)
     for k in ("params", "moments", "node_norm", "edge_norm"):
-        for a, b in zip(after[k], before[k]):
-            assert torch.equal(a, b), k
+        assert _same(after[k], before[k]), k
     assert (after["step_count"], after["lr"], after["last_epoch"]) == \
         (before["step_count"], before["lr"], before["last_epoch"])
     # output normaliser: exactly one accumulation of the bad batch's target delta
-    cnt_b, cnt_a = before["out_norm"][2], after["out_norm"][2]
-    assert float(cnt_a - cnt_b) == float(good.x.shape[0])
+    ob, oa = before["out_norm"], after["out_norm"]
+    assert float(oa["_acc_count"] - ob["_acc_count"]) == float(good.x.shape[0])
+    assert float(oa["_num_accumulations"] - ob["_num_accumulations"]) == 1.0
     delta = (good.y - good.x[:, 0:2]).double()
-    torch.testing.assert_close((after["out_norm"][0] - before["out_norm"][0]).double().reshape(-1),
-                               delta.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close((oa["_acc_sum"] - ob["_acc_sum"]).double().reshape(-1), delta.sum(0),
+                               rtol=1e-4, atol=1e-3)
     # recovery: a good batch trains on (same as a fresh run whose output normaliser saw the bad batch)
     st.batch = good
     loss = st()
@@ -192,11 +201,11 @@ def test_bad_edge_index_skips_the_optimizer_update():
             torch.cuda.synchronize()
     after = _state(sim, opt, sch)
     for k in ("params", "moments"):
-        for a, b in zip(after[k], before[k]):
-            assert torch.equal(a, b), k
+        assert _same(after[k], before[k]), k
     assert (after["step_count"], after["lr"], after["last_epoch"]) == \
         (before["step_count"], before["lr"], before["last_epoch"])
-    assert float(after["node_norm"][2] - before["node_norm"][2]) >= good.x.shape[0]
+    # the bad step's own preamble accumulated (before the topology build flagged the index)
+    assert float(after["node_norm"]["_acc_count"] - before["node_norm"]["_acc_count"]) == float(good.x.shape[0])
 
 
 def test_new_batch_in_graph_mode_is_replayed():
