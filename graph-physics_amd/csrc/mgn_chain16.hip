@@ -22,7 +22,8 @@
 // Diagnostics builds only (-DMGN_ABLATE=bits, results wrong when nonzero; see mgn_mlp.hip): edge
 // forward 1 = P gathers from row 0 (cache-resident), 2 = no P loads, 4 = no weight-staging loads,
 // 8 = no stores of outputs / saves; node forward 16 = no aggregation gathers; node kernels 32 = every
-// global weight fragment read from fragment 0 (L1-hot: the cost of streaming them from L2)
+// global weight fragment read from fragment 0 (L1-hot: the cost of streaming them from L2), 64 = the
+// same for the hand-off's projection fragments only
 #ifndef MGN_ABLATE
 #define MGN_ABLATE 0
 #endif
@@ -30,6 +31,10 @@
 #define MGN_DIRECT_ROWS 0
 #endif
 
+
+#ifndef MGN_PROJ_HANDOFF
+#define MGN_PROJ_HANDOFF 1  // A/B builds: 0 = the tile wave computes the next block's projections itself
+#endif
 
 #ifndef MGN_NODE_AG
 #define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
@@ -758,8 +763,9 @@ __device__ __forceinline__ int gfrag_voff(int lane) {
     const int r = lane & 15, g = lane >> 4;
     return (r * 8 + 4 * (g & 1) + 16 * (g >> 1) * 8) * 2;  // bytes
 }
+template <int ABL = 32>
 __device__ __forceinline__ bf16x8 gfrag(__amdgpu_buffer_rsrc_t rs, int voff, int tile) {
-    const int so = (MGN_ABLATE & 32) ? 0 : tile * 64 * 8 * 2;  // bytes (ablation 32: one L1-hot fragment)
+    const int so = (MGN_ABLATE & ABL) ? 0 : tile * 64 * 8 * 2;  // bytes (ablation: one L1-hot fragment)
     const u32x2 lo = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so, 0));
     const u32x2 hi = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, so + 2 * 16 * 8 * 2, 0));
     const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
@@ -798,6 +804,58 @@ __device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, con
                                               const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
     gemm16(acc, W, 0, Bx, lane);
     gemm16_global(acc, Ba, pack, tile_of, lane);
+}
+
+// The next block's node projections P = [x·W0bᵀ + b0 ‖ x·W0cᵀ] of node tile `tile`, by a wave other
+// than the one that computed x_out (chain16_node_fwd_kernel's hand-off): half 0's 32 weight fragments
+// (k-steps 4..7 of the next edge MLP's layer-0 pack) are loaded BEFORE waiting for the tile, half
+// 1's stream in under half 0's MFMAs. The x_out rows are read with agent-scope loads (from L2: the
+// producing wave's stores completed before it set *flag).
+__device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int64_t tile, unsigned* flag, __bf16* scr,
+                                               int lane) {
+    const int g = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.pn_pack);
+    const int vo = gfrag_voff(lane), kst = a.pn_kst;
+    bf16x8 fr[4][8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) fr[s][t] = gfrag<64>(rs, vo, t * kst + 4 + s);
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
+    // B operand of x_out rows (as load_e): lane (m, g), k-step s: features 32s + 4g.. and 32s + 16 + 4g..
+    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
+    const unsigned long long* xr = reinterpret_cast<const unsigned long long*>(a.out + row * H + 4 * g);
+    bf16x8 Bx[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const unsigned long long lo = __hip_atomic_load(xr + 8 * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(xr + 8 * s + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32x4 w = {(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+        Bx[s] = __builtin_bit_cast(bf16x8, w);
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        f4 pacc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pacc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pacc[t] = mfma16(fr[s][t], Bx[s], pacc[t]);
+            if (half == 0) {  // this k-step's registers now take half 1's fragments
+#pragma unroll
+                for (int t = 0; t < 8; ++t) fr[s][t] = gfrag<64>(rs, vo, t * kst + 8 + s);
+            }
+        }
+        if (half == 0) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const float* b = a.pn_b0 + 16 * t + 4 * g;  // 4-byte aligned only
+                pacc[t] += f4{b[0], b[1], b[2], b[3]};
+            }
+        }
+        store_rows<true>(pacc, scr, a.pn_out + half * H, tile, a.M, lane, 2 * H);
+    }
 }
 
 // SAVE = false: inference — no aggregate, R8, mask, z or rden saves
@@ -869,10 +927,20 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     // second half of each workgroup stages the weights WHILE the first half runs its tile's phase A
     // (the staging burst hides behind the aggregation's gathers instead of preceding them).
     const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
+    // Projection hand-off (split launches with a chained next block): the NEXT block's node
+    // projections of tile-wave w's tile are computed by its partner w + NW/2, which idles after the
+    // staging otherwise. The partner loads its weight fragments (L2) while the tile wave runs phase A
+    // and the MLP, then waits for the tile's x_out (an LDS word the tile wave sets once its x_out
+    // stores have completed), reads those rows back (agent-scope loads: L2) and runs the 64 MFMAs —
+    // the fragment stream leaves the tile's critical path. Same fragments, same k order: P is
+    // bit-identical to the tile wave computing it.
+    const bool handoff = MGN_PROJ_HANDOFF && split && a.pn_out != nullptr;
+    unsigned* flags = reinterpret_cast<unsigned*>(smem + LDS_W + LDS_V + LDS_S);  // [NW/2] (the R region)
     bf16x8 xb[4];
     f4 agg[8];
     STAMP_DECL;
     if (split) {
+        if (threadIdx.x < NW / 2) flags[threadIdx.x] = 0u;
         if (wave >= NW / 2) {
             stage16<4, NW / 2 * 64>(W, a.wpack, a.woff, a.wks, false, threadIdx.x - NW / 2 * 64);
             fill_vec(threadIdx.x - NW / 2 * 64, NW / 2 * 64);
@@ -885,6 +953,12 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     }
     __syncthreads();
     STAMP(0);
+    if (handoff && wave >= NW / 2) {
+        const int pw = wave - NW / 2;
+        const int64_t pt = (int64_t)pw * gridDim.x + blockIdx.x;  // the partner's (only) tile
+        if (pt < a.ntiles) node_proj_partner(a, pt, flags + pw, scr, lane);
+        return;
+    }
     for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
         if (!split || tile != first) phase_a(tile, xb, agg);
         const int64_t row = tile * TR + m;
@@ -950,7 +1024,11 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                 acc[t][r] = fmaf(sc[r], acc[t][r] * rq, (float)xb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
-        if (a.pn_out) {
+        if (handoff) {
+            // x_out stores complete (at L2) before the partner is told to read them back
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(flags + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (a.pn_out) {
             // the NEXT block's node projections from this tile's x_out (bf16, the bits just stored):
             // P = [x·W0bᵀ + b0 ‖ x·W0cᵀ] of the next edge MLP (its layer-0 k-steps 4..7 / 8..11,
             // fragments from L2) — what node_proj_kernel would compute in a launch of its own

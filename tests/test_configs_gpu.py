@@ -303,8 +303,8 @@ def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out):
 
     torch.manual_seed(0)
     m = EncodeProcessDecode(mp, node_in, edge_in, out, h, compute_dtype=dtype).to(DEV)
-    xd = x.to(DEV).requires_grad_(True)
-    ed = ea.to(DEV).requires_grad_(True)
+    xd = x.to(DEV).detach().clone().requires_grad_(True)  # fresh leaves: never the fixture's tensors
+    ed = ea.to(DEV).detach().clone().requires_grad_(True)
     y = m(Data(x=xd, edge_index=ei, edge_attr=ed))
     (y * gy.to(DEV)).sum().backward()
     torch.cuda.synchronize()

@@ -377,6 +377,39 @@ def test_empty_edge_set_bf16_training():
     assert relerr(y, yr) < 5e-2
 
 
+@pytest.mark.parametrize("edge_in", [3, 4, 8])
+def test_encoder_input_gradients_bf16_h128(edge_in):
+    """Input gradients (x, edge_attr) through the chained bf16 encoder kernels (h=128; the edge
+    encoder gathers its rows in CSC order): no further from fp64 than 2 x PyTorch's bf16 autocast."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    g = torch.Generator().manual_seed(5)
+    n, e = 300, 2000
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(e, edge_in, generator=g)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    torch.manual_seed(0)
+    ref = O.OracleEPD(2, 11, edge_in, 2, 128)
+    xr, er = x.double().requires_grad_(True), ea.double().requires_grad_(True)
+    p64 = {k: v.detach().double() for k, v in ref.named_parameters()}
+    (O.encode_process_decode(xr, ei, er, p64, 2) * gy.double()).sum().backward()
+    xa, eab = x.clone().requires_grad_(True), ea.clone().requires_grad_(True)
+    pac = {k: v.detach().clone() for k, v in ref.named_parameters()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ya = O.encode_process_decode(xa, ei, eab, pac, 2)
+    (ya.float() * gy).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(2, 11, edge_in, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
+    xd, ed = x.to(DEV).requires_grad_(True), ea.to(DEV).requires_grad_(True)
+    (m(Data(x=xd, edge_index=ei.to(DEV), edge_attr=ed)) * gy.to(DEV)).sum().backward()
+    ex, eac_x = relerr(xd.grad, xr.grad), relerr(xa.grad, xr.grad)
+    ee, eac_e = relerr(ed.grad, er.grad), relerr(eab.grad, er.grad)
+    print(f"\nedge_in {edge_in}: x grad {ex:.3e} (autocast {eac_x:.3e}), edge_attr grad {ee:.3e} (autocast {eac_e:.3e})")
+    assert ex <= max(1e-2, 2 * eac_x) and ee <= max(1e-2, 2 * eac_e)
+
+
 def test_encoder_input_gradients():
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils.data import Data
