@@ -190,9 +190,17 @@ __device__ __forceinline__ bf16x8 wfrag(const __bf16* W, int l, int t, int s, in
     return *reinterpret_cast<const bf16x8*>(W + ((size_t)((l * 8 + t) * 4 + s) * 64 + lane) * 8);
 }
 
-__device__ __forceinline__ void gemm16(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane) {
+// acc = bias (LDS vector, features 16t + 4g..; nullptr: 0) + W_l · B: the bias rides in the MFMA
+// accumulator instead of one v_add per output element after it
+__device__ __forceinline__ void acc_init(f4 (&acc)[8], const float* bias, int lane) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 8; ++t)
+        acc[t] = bias ? *reinterpret_cast<const f4*>(bias + 16 * t + 4 * (lane >> 4)) : f4{0.f, 0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ void gemm16(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane,
+                                       const float* bias = nullptr) {
+    acc_init(acc, bias, lane);
     // one k-step's 8 fragments in flight at a time (the other wave on the SIMD covers the LDS
     // latency); without the fence the scheduler hoists all 32 reads and the backward spills
 #pragma unroll
@@ -213,10 +221,10 @@ struct StoreDst {
 };
 
 __device__ __forceinline__ void gemm16_st(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane,
-                                          __bf16* scr, StoreDst d, int64_t tile, int64_t M) {
+                                          __bf16* scr, StoreDst d, int64_t tile, int64_t M,
+                                          const float* bias = nullptr) {
     const int m = lane & 15, g = lane >> 4;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    acc_init(acc, bias, lane);
     u32x2 rv[8];
     u32x4 rw[2];
     auto write = [&](int u) {
@@ -489,17 +497,18 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
             if (l == 0)
                 gemm16(acc, W, 0, in.eb, lane);
             else if (SAVE)
-                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M, vec + l * H);
             else
-                gemm16(acc, W, l, B, lane);
+                gemm16(acc, W, l, B, lane, vec + l * H);
             STAMP(2);
             unsigned bits = 0u;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                const f4 b = l == 0 ? bf4(pi[t]) + bf4(pj[t]) : *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
+                // layer 0: + P_i[dst] + P_j[src] (b0 folded into P_i); layers 1, 2: the bias is in acc
+                const f4 b = l == 0 ? bf4(pi[t]) + bf4(pj[t]) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float v = fmaxf(acc[t][r] + b[r], 0.f);
+                    const float v = fmaxf(l == 0 ? acc[t][r] + b[r] : acc[t][r], 0.f);
                     acc[t][r] = v;
                     bits = push_bit(bits, v);
                 }
@@ -510,21 +519,15 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         }
         // layer 3 (stores its input, the R8 save of layer 3) + RMSNorm + residual
         if (SAVE)
-            gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+            gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M, vec + 3 * H);
         else
-            gemm16(acc, W, 3, B, lane);
+            gemm16(acc, W, 3, B, lane, vec + 3 * H);
         STAMP(4);
         float ss = 0.f;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+        for (int t = 0; t < 8; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float z = acc[t][r] + b[r];
-                acc[t][r] = z;
-                ss = fmaf(z, z, ss);
-            }
-        }
+            for (int r = 0; r < 4; ++r) ss = fmaf(acc[t][r], acc[t][r], ss);  // z = acc (bias included)
         ss += __shfl_xor(ss, 16);
         ss += __shfl_xor(ss, 32);
         const float q = sqrtf(ss) * a.dinv + RMS_EPS;
@@ -801,8 +804,9 @@ __device__ __forceinline__ void gemm16_global(f4 (&acc)[8], const bf16x8 (&Ba)[4
 // node layer 0 = x block (LDS image, layer slot 0) + aggr block (global fragments)
 template <class TileFn>
 __device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, const bf16x8 (&Bx)[4],
-                                              const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane) {
-    gemm16(acc, W, 0, Bx, lane);
+                                              const bf16x8 (&Ba)[4], const __bf16* pack, TileFn tile_of, int lane,
+                                              const float* bias = nullptr) {
+    gemm16(acc, W, 0, Bx, lane, bias);
     gemm16_global(acc, Ba, pack, tile_of, lane);
 }
 
@@ -942,8 +946,16 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     if (split) {
         if (threadIdx.x < NW / 2) flags[threadIdx.x] = 0u;
         if (wave >= NW / 2) {
+#ifdef MGN_STAMPS
+            const unsigned long long s0 = __builtin_amdgcn_s_memtime();
+#endif
             stage16<4, NW / 2 * 64>(W, a.wpack, a.woff, a.wks, false, threadIdx.x - NW / 2 * 64);
             fill_vec(threadIdx.x - NW / 2 * 64, NW / 2 * 64);
+#ifdef MGN_STAMPS
+            lds_fence();
+            if (blockIdx.x == 0 && threadIdx.x == NW / 2 * 64)
+                printf("nfwd16_stage %llu\n", __builtin_amdgcn_s_memtime() - s0);
+#endif
         } else if (tile < a.ntiles) {
             phase_a(tile, xb, agg);
         }
@@ -951,6 +963,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         stage16(W, a.wpack, a.woff, a.wks, false);
         fill_vec(threadIdx.x, NW * 64);
     }
+    STAMP(4);  // wave 0: its phase A (split launches)
     __syncthreads();
     STAMP(0);
     if (handoff && wave >= NW / 2) {
@@ -973,18 +986,17 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         for (int l = 0; l < 3; ++l) {
             if (l == 0)
                 gemm16_layer0(acc, W, xb, Ba, a.wpack + a.woff[0],
-                              [](int t, int s) { return t * 8 + 4 + s; }, lane);
+                              [](int t, int s) { return t * 8 + 4 + s; }, lane, vec);
             else if (SAVE)  // stores its input (the R8 save of layer l) under the MFMAs
-                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M, vec + l * H);
             else
-                gemm16(acc, W, l, B, lane);
+                gemm16(acc, W, l, B, lane, vec + l * H);
             unsigned bits = 0u;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                const f4 b = *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float val = fmaxf(acc[t][r] + b[r], 0.f);
+                    const float val = fmaxf(acc[t][r], 0.f);  // bias in the accumulator
                     acc[t][r] = val;
                     bits = push_bit(bits, val);
                 }
@@ -993,21 +1005,15 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
             if (SAVE) a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
         }
         if (SAVE)
-            gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+            gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M, vec + 3 * H);
         else
-            gemm16(acc, W, 3, B, lane);
+            gemm16(acc, W, 3, B, lane, vec + 3 * H);
         STAMP(2);
         float ss = 0.f;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+        for (int t = 0; t < 8; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float z = acc[t][r] + b[r];
-                acc[t][r] = z;
-                ss = fmaf(z, z, ss);
-            }
-        }
+            for (int r = 0; r < 4; ++r) ss = fmaf(acc[t][r], acc[t][r], ss);  // z = acc (bias included)
         ss += __shfl_xor(ss, 16);
         ss += __shfl_xor(ss, 32);
         const float q = sqrtf(ss) * a.dinv + RMS_EPS;
@@ -1298,18 +1304,18 @@ __global__ __launch_bounds__(NW * 64) void chain16_dense_fwd_kernel(ChainDenseFw
 #pragma unroll
         for (int l = 0; l < 3; ++l) {
             if (l == 0) {
+                acc_init(acc, vec, lane);
 #pragma unroll
-                for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, 0, t, 0, lane), in0, f4{0.f, 0.f, 0.f, 0.f});
+                for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, 0, t, 0, lane), in0, acc[t]);
             } else {
-                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M);
+                gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M, vec + l * H);
             }
             unsigned bits = 0u;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
-                const f4 b = *reinterpret_cast<const f4*>(vec + l * H + 16 * t + 4 * g);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float v = fmaxf(acc[t][r] + b[r], 0.f);
+                    const float v = fmaxf(acc[t][r], 0.f);  // bias in the accumulator
                     acc[t][r] = v;
                     bits = push_bit(bits, v);
                 }
@@ -1317,18 +1323,12 @@ __global__ __launch_bounds__(NW * 64) void chain16_dense_fwd_kernel(ChainDenseFw
             to_operand(acc, B);
             a.mask32[l * a.mask_stride * 2 + tile * 64 + lane] = bits;
         }
-        gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M);
+        gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M, vec + 3 * H);
         float ss = 0.f;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const f4 b = *reinterpret_cast<const f4*>(vec + 3 * H + 16 * t + 4 * g);
+        for (int t = 0; t < 8; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float z = acc[t][r] + b[r];
-                acc[t][r] = z;
-                ss = fmaf(z, z, ss);
-            }
-        }
+            for (int r = 0; r < 4; ++r) ss = fmaf(acc[t][r], acc[t][r], ss);  // z = acc (bias included)
         ss += __shfl_xor(ss, 16);
         ss += __shfl_xor(ss, 32);
         const float q = sqrtf(ss) * a.dinv + RMS_EPS;
@@ -1529,7 +1529,7 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
     layer_offsets(m, a.woff, a.wks);
     for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.M = M;
     a.ntiles = rows_pad(M) / TR;  // every padded row: R8 saves and masks cover rows_pad(M)
     a.out = reinterpret_cast<__bf16*>(out);
@@ -1568,7 +1568,7 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.z_save = reinterpret_cast<const __bf16*>(sv->z);
     a.rden_save = sv->rden;
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
@@ -1644,7 +1644,7 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
     layer_offsets(m, a.woff, a.wks);
     for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.M = M;
     a.ntiles = rows_pad(M) / TR;
     a.out = reinterpret_cast<__bf16*>(x_out);
@@ -1672,7 +1672,7 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     a.z_save = reinterpret_cast<const __bf16*>(sv->z);
     a.rden_save = sv->rden;
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);
@@ -1726,7 +1726,7 @@ int chain16_dense_forward(const mgn_mlp* m, const void* in, int in_dtype, int64_
     layer_offsets(m, a.woff, a.wks);
     for (int l = 0; l < 4; ++l) a.bias[l] = m->bias[l];
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.M = M;
     a.ntiles = rows_pad(M) / TR;
     a.out = out;
@@ -1753,7 +1753,7 @@ int chain16_dense_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv,
     a.z_save = reinterpret_cast<const __bf16*>(sv->z);
     a.rden_save = sv->rden;
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)H));
+    a.dinv = norm_dinv(m);
     a.mask32 = reinterpret_cast<const unsigned*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     a.wtpack = reinterpret_cast<const __bf16*>(m->wtpack);

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
+#include <cmath>
 
 #include <string>
 
@@ -174,6 +176,9 @@ __host__ __device__ __forceinline__ int64_t r8_index(int64_t m, int64_t c, int64
 }
 // Saved buffers cover rows padded to 64 (every tile, including pure-padding rows, is written).
 // compute units of the current device (read once; 256 on MI355X)
+// CUs the persistent kernels size their grids for. MGN_MAX_CUS (read once) caps it, so two streams
+// can each run a persistent kernel on part of the chip at the same time (intra-GPU data parallelism
+// experiments: tools/exp_dual.py).
 inline int device_cus() {
     static int cus = 0;
     if (cus == 0) {
@@ -183,10 +188,19 @@ inline int device_cus() {
             cus = n;
         else
             cus = 256;
+        if (const char* e = getenv("MGN_MAX_CUS")) {
+            const int c = atoi(e);
+            if (c > 0 && c < cus) cus = c;
+        }
     }
     return cus;
 }
 __host__ __device__ __forceinline__ int64_t rows_pad(int64_t M) { return (M + 63) / 64 * 64; }
+// RMSNorm's d^(-1/2) (layers.py:59-74) of an MLP: the true feature count (norm_dim) of a padded MLP
+inline float norm_dinv(const mgn_mlp* m) {
+    const int d = m->norm_dim > 0 ? m->norm_dim : m->out_dim;
+    return (float)(1.0 / sqrt((double)d));
+}
 __host__ __device__ __forceinline__ int kstep_of(int dtype) { return dtype == MGN_BF16 ? 32 : 4; }
 // R8 column count of the saved INPUT of layer l (layer 0: padded MLP input; else padded hidden)
 __host__ __device__ inline int act_cols(const mgn_mlp& m, int l) {

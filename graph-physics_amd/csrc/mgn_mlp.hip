@@ -1398,6 +1398,15 @@ __global__ __launch_bounds__(MGN_THREADS) void wgrad_reduce_kernel(RedArgs a) {
 }
 
 // --------------------------------------------------------------------------- weight packing
+// element (nn, kk) of a job's (possibly zero-padded) [n][k] matrix
+__device__ __forceinline__ float pack_src(const mgn_pack_job& j, int nn, int kk) {
+    if (j.kb_pad <= 0) return j.w[(int64_t)nn * j.k + kk];  // unpadded
+    if (nn >= j.n_src) return 0.f;
+    const int b = kk / j.kb_pad, c = kk - b * j.kb_pad;
+    const int sc = b * j.kb_src + c;
+    return c < j.kb_src && sc < j.k_src ? j.w[(int64_t)nn * j.k_src + sc] : 0.f;
+}
+
 template <class T>
 __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
@@ -1419,7 +1428,7 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
             if (tile < NTp * KS) {
                 const int nt = tile / KS, ks = tile % KS;
                 const int nn = nt * 16 + (lane & 15), kk = ks * KSTEP + VEC * (lane >> 4) + v;
-                if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
+                if (nn < n && kk < k) w = pack_src(j, nn, kk);
             }
             dst[e] = from_f<T>(w);
         }
@@ -1428,7 +1437,7 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
             if (tile < KTp * NS) {
                 const int kt = tile / NS, ns = tile % NS;
                 const int kk = kt * 16 + (lane & 15), nn = ns * KSTEP + VEC * (lane >> 4) + v;
-                if (nn < n && kk < k) w = j.w[(int64_t)nn * k + kk];
+                if (nn < n && kk < k) w = pack_src(j, nn, kk);
             }
             dstT[e] = from_f<T>(w);
         }
@@ -1478,7 +1487,9 @@ int check_mlp(const mgn_mlp* m) {
     MGN_REQUIRE(m->n_layers >= 2 && m->n_layers <= MGN_MAX_LAYERS,
                 "The MLP must have at least 2 layers (input and output) and at most 8");
     MGN_REQUIRE(m->hidden == 16 || m->hidden == 32 || m->hidden == 64 || m->hidden == 128,
-                "hidden size must be one of 16, 32, 64, 128");
+                "kernel width (mgn_mlp.hidden) must be 16, 32, 64 or 128; a model of another hidden size "
+                "<= 128 runs zero-padded to the next width with norm_dim = its true size");
+    MGN_REQUIRE(m->norm_dim >= 0 && m->norm_dim <= m->out_dim, "norm_dim must be in [0, out_dim]");
     MGN_REQUIRE(m->in_dim >= 1, "in_dim must be >= 1");
     MGN_REQUIRE(m->out_dim == m->hidden || (m->out_dim >= 1 && m->out_dim <= 16),
                 "out_dim must equal hidden or be in [1, 16]");
@@ -1524,7 +1535,7 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     a.wpack = m->wpack;
     for (int l = 0; l < m->n_layers; ++l) a.bias[l] = m->bias[l];
     a.scale = m->scale;
-    a.dinv = (float)(1.0 / sqrt((double)m->out_dim));
+    a.dinv = norm_dinv(m);
     if (MODE == MODE_NODE) {
         a.seg_ptr = topo->col_ptr;
         a.agg_z = agg_sv->z;
@@ -1585,7 +1596,7 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     a.has_norm = m->has_norm;
     a.ldh = pad_ld<T>(rup(H, Mf<T>::KSTEP));
     a.mode = MODE;
-    a.dinv = (float)(1.0 / sqrt((double)m->out_dim));
+    a.dinv = norm_dinv(m);
     a.wtpack = m->wtpack;
     a.scale = m->scale;
     a.mask = reinterpret_cast<const unsigned long long*>(sv->mask);

@@ -36,8 +36,8 @@ class Topology(ctypes.Structure):
 
 class Mlp(ctypes.Structure):
     _fields_ = [("n_layers", _i32), ("in_dim", _i32), ("hidden", _i32), ("out_dim", _i32),
-                ("has_norm", _i32), ("dtype", _i32), ("wpack", _vp), ("wtpack", _vp),
-                ("bias", _vp * MGN_MAX_LAYERS), ("scale", _vp)]
+                ("has_norm", _i32), ("dtype", _i32), ("norm_dim", _i32), ("reserved", _i32),
+                ("wpack", _vp), ("wtpack", _vp), ("bias", _vp * MGN_MAX_LAYERS), ("scale", _vp)]
 
 
 class MlpSaved(ctypes.Structure):
@@ -59,8 +59,8 @@ class NormalizerState(ctypes.Structure):
 
 
 class PackJob(ctypes.Structure):
-    _fields_ = [("w", _vp), ("dst", _vp), ("dstT", _vp), ("n", _i32), ("k", _i32),
-                ("dtype", _i32), ("reserved", _i32)]
+    _fields_ = [("w", _vp), ("dst", _vp), ("dstT", _vp), ("n", _i32), ("k", _i32), ("dtype", _i32),
+                ("n_src", _i32), ("k_src", _i32), ("kb_src", _i32), ("kb_pad", _i32), ("reserved", _i32)]
 
 
 EXPORTS = {

@@ -117,8 +117,25 @@ def get_topology(edge_index, num_nodes):
 
 
 # --------------------------------------------------------------------------- MLPs and plans
+KERNEL_WIDTHS = (16, 32, 64, 128)
+
+
+def kernel_width(h):
+    """The hidden width libmgn's kernels run a model of hidden size h on: h itself when the kernels
+    are instantiated for it, else the next such width with zero-padded channels (exact: padded
+    weights, biases and RMSNorm scales are 0, so every padded channel stays 0 forward and backward,
+    and the RMSNorm divides by the true h — mgn_mlp.norm_dim). Above 128: unsupported."""
+    for w in KERNEL_WIDTHS:
+        if h <= w:
+            return w
+    raise ValueError(f"hidden_size {h} is not supported by libmgn's kernels (at most {KERNEL_WIDTHS[-1]})")
+
+
 class MlpSpec:
-    def __init__(self, seq):
+    """kblocks: layer 0's input is kblocks blocks of `hidden` features ([e ‖ x_i ‖ x_j]: 3, [x ‖ aggr]: 2),
+    each padded to the kernel width; 0: a raw input (encoders) whose columns are not padded."""
+
+    def __init__(self, seq, kblocks=0):
         from graphphysics.models.layers import RMSNorm
 
         mods = list(seq)
@@ -145,45 +162,100 @@ class MlpSpec:
         if self.norm is not None:
             self.params.append(self.norm.scale)
         self.numel = sum(p.numel() for p in self.params)
+        # kernel geometry (zero-padded when the hidden size is not a kernel width)
+        self.width = kernel_width(self.hidden)
+        self.padded = self.width != self.hidden
+        if kblocks and self.in_dim != kblocks * self.hidden:
+            raise ValueError("block MLP input must be %d x hidden" % kblocks)
+        self.kblocks = kblocks
+        pad_n = lambda n: self.width if n == self.hidden else n  # noqa: E731 (hidden rows padded; the decoder's out not)
+        self.shapes = []  # per Linear: (n_pad, k_pad, n, k, kb_src, kb_pad)
+        for i, lin in enumerate(linears):
+            n, k = lin.out_features, lin.in_features
+            if i == 0:
+                kp, kbs, kbp = (kblocks * self.width, self.hidden, self.width) if kblocks else (k, 0, 0)
+            else:
+                kp, kbs, kbp = self.width, self.hidden, self.width
+            self.shapes.append((pad_n(n), kp, n, k, kbs, kbp))
+        self.out_width = pad_n(self.out_dim)
+        # parameter layout of the padded MLP (what the kernels' gradients are written in)
+        self.numel_pad = sum(np_ * kp + np_ for np_, kp, *_ in self.shapes) + (self.out_width if self.norm else 0)
 
-    def describe(self, mdt, wpack, wtpack):
+    def describe(self, mdt, wpack, wtpack, bias_ptrs=None, scale_ptr=None):
         d = nat.Mlp()
-        d.n_layers, d.in_dim, d.hidden, d.out_dim = self.n_layers, self.in_dim, self.hidden, self.out_dim
+        d.n_layers, d.in_dim, d.hidden, d.out_dim = self.n_layers, self.shapes[0][1], self.width, self.out_width
         d.has_norm, d.dtype = int(self.norm is not None), mdt
+        d.norm_dim = self.out_dim if (self.padded and self.norm is not None) else 0
         d.wpack, d.wtpack = wpack, wtpack
         for i, lin in enumerate(self.linears):
-            d.bias[i] = lin.bias.data_ptr()
-        d.scale = self.norm.scale.data_ptr() if self.norm is not None else 0
+            d.bias[i] = bias_ptrs[i] if bias_ptrs is not None else lin.bias.data_ptr()
+        if self.norm is not None:
+            d.scale = scale_ptr if scale_ptr is not None else self.norm.scale.data_ptr()
+        else:
+            d.scale = 0
         return d
 
 
 class _PackedWeights:
-    """Fragment-packed copies of all Linear weights of a plan for one (device, dtype)."""
+    """Fragment-packed copies of all Linear weights of a plan for one (device, dtype); for a plan with
+    zero-padded MLPs also the padded fp32 biases / RMSNorm scales the kernels read (refreshed with the
+    packs every forward: one gather launch)."""
 
     def __init__(self, plan, device, mdt):
         L = nat.lib()
         tdt = nat.torch_dtype(mdt)
         regions, jobs, total, max_el = [], [], 0, 1
         for spec in plan.specs:
-            per = [int(L.mgn_linear_pack_elems(lin.out_features, lin.in_features, mdt))
-                   for lin in spec.linears]
+            per = [int(L.mgn_linear_pack_elems(np_, kp, mdt)) for np_, kp, *_ in spec.shapes]
             regions.append((total, per))
             total += 2 * sum(per)
         self.buf = torch.empty(max(total, 1), dtype=tdt, device=device)
         esz = self.buf.element_size()
         base = self.buf.data_ptr()
+        # padded bias / scale vectors: pad_vec[i] = flat_params[pad_idx[i]] (pad_idx -1: 0)
+        self.pad_vec = None
+        vec_slots = []
+        if any(sp.padded for sp in plan.specs):
+            flat = plan.module._flat_params
+            f0 = flat.storage_offset()
+            idx = []
+            for sp in plan.specs:
+                if not sp.padded:
+                    continue
+                vecs = [lin.bias for lin in sp.linears] + ([sp.norm.scale] if sp.norm is not None else [])
+                widths = [s_[0] for s_ in sp.shapes] + ([sp.out_width] if sp.norm is not None else [])
+                for v, w in zip(vecs, widths):
+                    o = v.storage_offset() - f0
+                    vec_slots.append(len(idx))
+                    idx += [o + i if i < v.numel() else -1 for i in range(w)]
+            pidx = torch.tensor(idx, dtype=torch.int64)
+            self.pad_mask = (pidx >= 0).to(device=device, dtype=torch.float32)
+            self.pad_idx = pidx.clamp(min=0).to(device)
+            self.pad_vec = torch.zeros(len(idx), dtype=torch.float32, device=device)
+            self.pad_tmp = torch.zeros_like(self.pad_vec)
+            self.flat = flat
+        vbase = self.pad_vec.data_ptr() if self.pad_vec is not None else 0
+        slot = iter(vec_slots)
         self.descs = []
         for spec, (off, per) in zip(plan.specs, regions):
             n = sum(per)
             wp, wtp = base + off * esz, base + (off + n) * esz
             o = 0
-            for lin, cnt in zip(spec.linears, per):
-                j = nat.PackJob(lin.weight.data_ptr(), wp + o * esz, wtp + o * esz,
-                                lin.out_features, lin.in_features, mdt, 0)
+            for lin, cnt, (np_, kp, n0, k0, kbs, kbp) in zip(spec.linears, per, spec.shapes):
+                if spec.padded:
+                    j = nat.PackJob(lin.weight.data_ptr(), wp + o * esz, wtp + o * esz, np_, kp, mdt,
+                                    n0, k0, kbs if kbp else k0, kbp if kbp else k0, 0)
+                else:
+                    j = nat.PackJob(lin.weight.data_ptr(), wp + o * esz, wtp + o * esz, np_, kp, mdt, 0, 0, 0, 0, 0)
                 jobs.append(j)
-                max_el = max(max_el, lin.out_features * lin.in_features)
+                max_el = max(max_el, np_ * kp)
                 o += cnt
-            self.descs.append(spec.describe(mdt, wp, wtp))
+            if spec.padded:
+                bptr = [vbase + 4 * next(slot) for _ in spec.linears]
+                sptr = vbase + 4 * next(slot) if spec.norm is not None else None
+                self.descs.append(spec.describe(mdt, wp, wtp, bptr, sptr))
+            else:
+                self.descs.append(spec.describe(mdt, wp, wtp))
         arr = (nat.PackJob * len(jobs))(*jobs)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self.jobs = raw.to(device)
@@ -192,14 +264,17 @@ class _PackedWeights:
 
     def repack(self, stream):
         nat.check(nat.lib().mgn_pack_weights(nat.ptr(self.jobs), self.njobs, self.max_el, stream))
+        if self.pad_vec is not None:
+            torch.index_select(self.flat.detach(), 0, self.pad_idx, out=self.pad_tmp)
+            torch.mul(self.pad_tmp, self.pad_mask, out=self.pad_vec)
 
 
 class ModelPlan:
-    """All MLPs of a module, in module.parameters() order."""
+    """All MLPs of a module, in module.parameters() order. kblocks: per MLP (MlpSpec)."""
 
-    def __init__(self, module, mlps):
+    def __init__(self, module, mlps, kblocks=None):
         self.module = module
-        self.specs = [MlpSpec(m) for m in mlps]
+        self.specs = [MlpSpec(m, kb) for m, kb in zip(mlps, kblocks or [0] * len(mlps))]
         order = [p for s in self.specs for p in s.params]
         mine = list(module.parameters())
         if len(order) != len(mine) or any(a is not b for a, b in zip(order, mine)):
@@ -211,7 +286,36 @@ class ModelPlan:
             self.offsets.append(o)
             o += s.numel
         self.numel = o
+        # zero-padded MLPs: the kernels write gradients in the padded layout (offsets_pad / numel_pad);
+        # unpad_idx gathers the true gradients from it
+        self.padded = any(s.padded for s in self.specs)
+        self.offsets_pad, self.numel_pad = list(self.offsets), self.numel
+        self.unpad_idx = None
+        if self.padded:
+            self.offsets_pad, idx, o = [], [], 0
+            for s in self.specs:
+                self.offsets_pad.append(o)
+                for lin, (np_, kp, n, k, kbs, kbp) in zip(s.linears, s.shapes):
+                    # weight [n][k] inside [np_][kp] (k: blocks of kbs source columns in kbp)
+                    c = torch.arange(k)
+                    col = (c // kbs) * kbp + c % kbs if kbp else c
+                    idx.append((o + torch.arange(n)[:, None] * kp + col[None, :]).reshape(-1))
+                    o += np_ * kp
+                    idx.append(o + torch.arange(n))  # bias
+                    o += np_
+                if s.norm is not None:
+                    idx.append(o + torch.arange(s.out_dim))
+                    o += s.out_width
+            self.numel_pad = o
+            self._unpad_cpu = torch.cat(idx).to(torch.int64)
+            assert self._unpad_cpu.numel() == self.numel
         self._packed = {}
+
+    def unpad(self, Gp):
+        """True-layout gradients from the padded layout (one gather)."""
+        if self.unpad_idx is None or self.unpad_idx.device != Gp.device:
+            self.unpad_idx = self._unpad_cpu.to(Gp.device)
+        return torch.index_select(Gp, 0, self.unpad_idx)
 
     def packed(self, device, mdt):
         key = (str(device), mdt)
@@ -263,7 +367,7 @@ def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
                                             ctypes.byref(mw)))
     act = _empty(ae.value, tdt, device)
     mask = _empty(mw.value, torch.int64, device)
-    z = _empty(rows * spec.hidden, tdt, device) if need_z else None
+    z = _empty(rows * spec.width, tdt, device) if need_z else None
     rden = _empty(rows, torch.float32, device) if need_z else None
     s = nat.MlpSaved(act.data_ptr(), mask.data_ptr(), z.data_ptr() if z is not None else 0,
                      rden.data_ptr() if rden is not None else 0)
@@ -273,16 +377,21 @@ def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
 def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device):
     se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True, True)
     sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None, True)
-    aggr = _empty(topo.num_nodes * espec.hidden, tdt, device)
+    aggr = _empty(topo.num_nodes * espec.width, tdt, device)
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
 
 
 def _alloc_block_infer(espec, topo, tdt, device):
     """Inference scratch of mgn_block_forward (act = NULL): the edge MLP's z/rden only."""
-    z = _empty(topo.num_edges * espec.hidden, tdt, device)
+    z = _empty(topo.num_edges * espec.width, tdt, device)
     rden = _empty(topo.num_edges, torch.float32, device)
     se = nat.MlpSaved(0, 0, z.data_ptr(), rden.data_ptr())
     return nat.BlockSaved(se, nat.MlpSaved(0, 0, 0, 0), 0), (z, rden)
+
+
+def _padc(t, H):
+    """Columns zero-padded to the kernel width H (no copy when already H wide)."""
+    return t if t.shape[1] == H else torch.nn.functional.pad(t, (0, H - t.shape[1]))
 
 
 def _permute(src, idx, rows, cols, in_mdt, out_tdt, scatter, stream, out=None):
@@ -346,16 +455,16 @@ class EPDFunction(torch.autograd.Function):
         train = any(ctx.needs_input_grad)
         if only_processor:
             bspecs, bdescs = plan.specs, descs
-            H = bspecs[0].hidden
-            x0 = x.detach().to(tdt).contiguous()
-            e0 = _permute(edge_attr.detach().float().contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt,
+            H = bspecs[0].width  # the kernels' width (zero-padded when != hidden_size)
+            x0 = _padc(x.detach(), H).to(tdt).contiguous()
+            e0 = _permute(_padc(edge_attr.detach().float(), H).contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt,
                           False, st)
             sv_ne = sv_ee = sv_dec = None
             xin = ein = None
         else:
             bspecs, bdescs = plan.specs[3:], descs[3:]
             ne, ee, dec = plan.specs[:3]
-            H = ne.hidden
+            H = ne.width
             xin = x.detach().float().contiguous()
             ein = edge_attr.detach().float().contiguous()
             x0 = torch.empty((N, H), dtype=tdt, device=dev)
@@ -401,11 +510,13 @@ class EPDFunction(torch.autograd.Function):
             else:
                 xs, es = [x1], [e1]
         if only_processor:
-            out = xs[-1].float()
+            out = xs[-1][:, :bspecs[0].hidden].float().contiguous()
         else:
-            out = torch.empty((N, dec.out_dim), dtype=torch.float32, device=dev)
+            out = torch.empty((N, dec.out_width), dtype=torch.float32, device=dev)
             sv_dec = _alloc_mlp_saved(descs[2], dec, N, tdt, dev, dec.norm is not None)
             _mlp_fwd(descs[2], dec, xs[-1], mdt, H, None, N, out, nat.MGN_F32, sv_dec[0], st)
+            if dec.out_width != dec.out_dim:  # a decoder whose output width is the (padded) hidden size
+                out = out[:, :dec.out_dim].contiguous()
         if train:
             ctx.plan, ctx.mdt, ctx.only_processor, ctx.topo = plan, mdt, only_processor, topo
             ctx.pw = pw
@@ -422,9 +533,13 @@ class EPDFunction(torch.autograd.Function):
         tdt = nat.torch_dtype(mdt)
         N, E, H = topo.num_nodes, topo.num_edges, ctx.H
         descs = pw.descs
-        G = torch.empty(plan.numel, dtype=torch.float32, device=dev)
+        # the kernels write gradients in the (zero-)padded parameter layout; a plan of kernel-width
+        # MLPs has the true layout (offsets_pad == offsets, no gather at the end)
+        G = torch.empty(plan.numel_pad, dtype=torch.float32, device=dev)
         gp = G.data_ptr()
-        off = plan.offsets
+        off = plan.offsets_pad
+        # gradient-ready ranges are in the true layout: a padded plan hands over everything at the end
+        ready = (lambda *_: None) if plan.padded else _grad_ready
         if ctx.only_processor:
             bdescs, boff = descs, off
         else:
@@ -435,13 +550,13 @@ class EPDFunction(torch.autograd.Function):
                        _ws_bytes_mlp(descs[2], N))
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
         if ctx.only_processor:
-            dx = gout.detach().to(tdt).contiguous()
+            dx = _padc(gout.detach(), H).to(tdt).contiguous()
         else:
             dx = torch.empty((N, H), dtype=tdt, device=dev)
-            g = gout.detach().float().contiguous()
+            g = _padc(gout.detach().float(), plan.specs[2].out_width).contiguous()
             _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                      ctypes.c_void_p(gp + 4 * off[2]), ws, st)
-            _grad_ready(G, off[2], off[2] + plan.specs[2].numel)
+            ready(G, off[2], off[2] + plan.specs[2].numel)
         nb = len(bdescs) // 2
         # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
         # gradient is zero, which the chained bf16 kernels take as NULL (no zero fill, no reads)
@@ -501,7 +616,7 @@ class EPDFunction(torch.autograd.Function):
                     if (pend_hi - boff[2 * b]) * 4 >= GRAD_GROUP_BYTES or b == 0:
                         # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
                         nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1), st))
-                        _grad_ready(G, boff[2 * b], pend_hi)
+                        ready(G, boff[2 * b], pend_hi)
                         pend_hi = pend_b = None
             elif not overlap:
                 if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
@@ -510,7 +625,7 @@ class EPDFunction(torch.autograd.Function):
                                                              st))
                 else:
                     nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
-                _grad_ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
+                ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
             else:
                 w = wss[b % 2]
                 if done[b % 2] is not None:
@@ -533,10 +648,11 @@ class EPDFunction(torch.autograd.Function):
         gx = gea = None
         nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         if ctx.only_processor:
+            h = plan.specs[0].hidden
             if nx:
-                gx = dx.float()
+                gx = dx[:, :h].float().contiguous()
             if nea:
-                gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)
+                gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous()
         else:
             ne, ee = plan.specs[0], plan.specs[1]
             gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
@@ -548,7 +664,10 @@ class EPDFunction(torch.autograd.Function):
             gx = gxc
             if nea:
                 gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
-            _grad_ready(G, off[0], off[1] + plan.specs[1].numel)
+            ready(G, off[0], off[1] + plan.specs[1].numel)
+        if plan.padded:
+            G = plan.unpad(G)
+            _grad_ready(G, 0, plan.numel)
         ctx.state = None
         return (None, None, None, gx, gea, None, *plan.grad_views(G))
 
@@ -565,16 +684,16 @@ class BlockFunction(torch.autograd.Function):
         pw = plan.packed(dev, mdt)
         pw.repack(st)
         espec, nspec = plan.specs
-        H = espec.hidden
+        h, H = espec.hidden, espec.width  # hidden size, kernel width (zero-padded when they differ)
         N, E = topo.num_nodes, topo.num_edges
-        x0 = x.detach().to(tdt).contiguous()
+        x0 = _padc(x.detach(), H).to(tdt).contiguous()
         ea = edge_attr.detach()
         if ea.dtype not in (torch.float32, torch.bfloat16):  # fp16 (autocast), fp64, ...: read as fp32
             ea = ea.float()
-        if ea.dim() != 2 or ea.shape[0] != E or ea.shape[1] != H:
-            raise ValueError(f"edge_attr must have shape [{E}, {H}], got {list(ea.shape)}")
-        e0 = _permute(ea.contiguous(), topo.csc_eid, E, H, nat.mgn_dtype(ea.dtype), tdt, False, st) if E else \
-            torch.empty((0, H), dtype=tdt, device=dev)
+        if ea.dim() != 2 or ea.shape[0] != E or ea.shape[1] != h:
+            raise ValueError(f"edge_attr must have shape [{E}, {h}], got {list(ea.shape)}")
+        e0 = _permute(_padc(ea, H).contiguous(), topo.csc_eid, E, H, nat.mgn_dtype(ea.dtype), tdt, False, st) \
+            if E else torch.empty((0, H), dtype=tdt, device=dev)
         train = any(ctx.needs_input_grad)
         if not train and nat.lib().mgn_block_forward_inference_supported(ctypes.byref(pw.descs[0]),
                                                                          ctypes.byref(pw.descs[1])):
@@ -593,6 +712,8 @@ class BlockFunction(torch.autograd.Function):
             ctx.plan, ctx.mdt, ctx.topo, ctx.pw = plan, mdt, topo, pw
             ctx.state = (x0, e0, sv)
             ctx.xdtype = x.dtype
+        if H != h:
+            return x1[:, :h].to(x.dtype).contiguous(), e_out[:, :h].contiguous()
         return x1.to(x.dtype), e_out
 
     @staticmethod
@@ -603,13 +724,14 @@ class BlockFunction(torch.autograd.Function):
         st = nat.stream_ptr(dev)
         tdt = nat.torch_dtype(mdt)
         N, E = topo.num_nodes, topo.num_edges
-        H = plan.specs[0].hidden
-        dxo = (gx if gx is not None else torch.zeros((N, H), device=dev)).detach().to(tdt).contiguous()
+        h, H = plan.specs[0].hidden, plan.specs[0].width
+        dxo = _padc((gx if gx is not None else torch.zeros((N, h), device=dev)).detach(), H).to(tdt).contiguous()
         if ge is None or E == 0:
             deo = torch.zeros((max(E, 1), H), dtype=tdt, device=dev)
         else:
-            deo = _permute(ge.detach().float().contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt, False, st)
-        G = torch.empty(plan.numel, dtype=torch.float32, device=dev)
+            deo = _permute(_padc(ge.detach().float(), H).contiguous(), topo.csc_eid, E, H, nat.MGN_F32, tdt, False,
+                           st)
+        G = torch.empty(plan.numel_pad, dtype=torch.float32, device=dev)
         ws = torch.empty(max(_ws_bytes_block(topo, pw.descs[0], pw.descs[1]), 1), dtype=torch.uint8,
                          device=dev)
         dx = torch.empty((N, H), dtype=tdt, device=dev)
@@ -617,12 +739,14 @@ class BlockFunction(torch.autograd.Function):
         nat.check(nat.lib().mgn_block_backward(
             ctypes.byref(topo.struct), ctypes.byref(pw.descs[0]), ctypes.byref(pw.descs[1]), nat.ptr(x0),
             nat.ptr(e0), ctypes.byref(sv[0]), nat.ptr(dxo), nat.ptr(deo), nat.ptr(dx), nat.ptr(de),
-            ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(G.data_ptr() + 4 * plan.offsets[1]),
+            ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(G.data_ptr() + 4 * plan.offsets_pad[1]),
             nat.ptr(ws), ws.numel(), st))
-        gxo = dx.to(ctx.xdtype) if ctx.needs_input_grad[2] else None
+        gxo = dx[:, :h].to(ctx.xdtype).contiguous() if ctx.needs_input_grad[2] else None
         geo = None
         if ctx.needs_input_grad[3]:
-            geo = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st) if E else \
-                torch.zeros((0, H), device=dev)
+            geo = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous() if E else \
+                torch.zeros((0, h), device=dev)
+        if plan.padded:
+            G = plan.unpad(G)
         ctx.state = None
         return (None, None, gxo, geo, None, *plan.grad_views(G))

@@ -223,7 +223,7 @@ class GraphNetBlock(nn.Module):
 
     def _get_plan(self):
         if self._plan is None:
-            self._plan = _engine.ModelPlan(self, [self.edge_block, self.node_block])
+            self._plan = _engine.ModelPlan(self, [self.edge_block, self.node_block], [3, 2])
         return self._plan
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, edge_attr: torch.Tensor,

@@ -60,9 +60,11 @@ class EncodeProcessDecode(nn.Module):
         if self._plan is None:
             mlps = [] if self.only_processor else [self.nodes_encoder, self.edges_encoder,
                                                    self.decode_module]
+            kblocks = [0] * len(mlps)
             for blk in self.processor_list:
                 mlps += [blk.edge_block, blk.node_block]
-            self._plan = _engine.ModelPlan(self, mlps)
+                kblocks += [3, 2]  # [e ‖ x_i ‖ x_j], [x ‖ aggr]: hidden-wide blocks
+            self._plan = _engine.ModelPlan(self, mlps, kblocks)
         return self._plan
 
     def forward(self, graph) -> torch.Tensor:

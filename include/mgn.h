@@ -107,10 +107,14 @@ int mgn_topology_build_async(const int64_t* edge_index, int64_t num_edges, int64
 typedef struct mgn_mlp {
     int32_t n_layers; /* number of nn.Linear (reference nb_of_layers, >= 2)                    */
     int32_t in_dim;   /* input features of Linear 0                                          */
-    int32_t hidden;   /* hidden width (16, 32, 64 or 128)                                    */
+    int32_t hidden;   /* hidden width the kernels run (16, 32, 64 or 128)                     */
     int32_t out_dim;  /* output features of the last Linear (== hidden, or 1..16)            */
     int32_t has_norm; /* RMSNorm(out_dim) after the last Linear                              */
     int32_t dtype;    /* MGN_F32 | MGN_BF16                                                  */
+    int32_t norm_dim; /* ABI v11: the RMSNorm's d in rms = |x|·d^(-1/2) (0: out_dim). A model of hidden
+                         size h the kernels do not instantiate runs on the next supported width with
+                         exactly-zero padded channels; its RMSNorm still divides by the true h      */
+    int32_t reserved;
     const void* wpack;  /* forward fragments, mgn_mlp_pack_elems() elements of dtype         */
     const void* wtpack; /* transposed fragments (backward), same element count                */
     const float* bias[MGN_MAX_LAYERS]; /* fp32 master biases                                  */
@@ -139,7 +143,12 @@ typedef struct mgn_pack_job {
     const float* w;
     void* dst;   /* forward fragments  */
     void* dstT;  /* transposed fragments */
-    int32_t n, k, dtype, reserved;
+    int32_t n, k, dtype;
+    /* ABI v11, zero-padded packs (0: none): the source w is [n_src][k_src] row-major, packed as the
+     * [n][k] matrix whose rows >= n_src are 0 and whose k axis is blocks of kb_pad columns holding
+     * kb_src source columns each (rest 0): e.g. [e ‖ x_i ‖ x_j] of hidden h on width H: kb_src = h,
+     * kb_pad = H */
+    int32_t n_src, k_src, kb_src, kb_pad, reserved;
 } mgn_pack_job;
 
 int64_t mgn_linear_pack_elems(int32_t n, int32_t k, int32_t dtype);

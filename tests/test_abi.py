@@ -58,6 +58,7 @@ int main(void) {
   printf("mgn_pack_job %zu\n", sizeof(mgn_pack_job));
   P(mgn_topology, row_perm) P(mgn_mlp, wpack) P(mgn_mlp, bias) P(mgn_mlp, scale)
   P(mgn_mlp_saved, rden) P(mgn_block_saved, node) P(mgn_block_saved, aggr) P(mgn_pack_job, n)
+  P(mgn_mlp, norm_dim) P(mgn_pack_job, n_src) P(mgn_pack_job, kb_pad)
   return 0;
 }
 """
@@ -81,6 +82,9 @@ int main(void) {
     assert int(got["mgn_block_saved.node"]) == nat.BlockSaved.node.offset
     assert int(got["mgn_block_saved.aggr"]) == nat.BlockSaved.aggr.offset
     assert int(got["mgn_pack_job.n"]) == nat.PackJob.n.offset
+    assert int(got["mgn_mlp.norm_dim"]) == nat.Mlp.norm_dim.offset
+    assert int(got["mgn_pack_job.n_src"]) == nat.PackJob.n_src.offset
+    assert int(got["mgn_pack_job.kb_pad"]) == nat.PackJob.kb_pad.offset
 
 
 def test_host_size_functions(lib):

@@ -150,12 +150,15 @@ def _cyl_graph():
     return n, torch.from_numpy(ei)
 
 
-@pytest.mark.parametrize("dtype,tf,tg", [(torch.float32, 1e-5, None), (torch.bfloat16, 1e-2, 1.5e-1)])
-def test_block_cylinder_h128_vs_oracle(dtype, tf, tg):
+@pytest.mark.parametrize("dtype,tf,tg,h", [(torch.float32, 1e-5, None, 128), (torch.bfloat16, 1e-2, 1.5e-1, 128),
+                                            (torch.float32, 1e-5, None, 96), (torch.bfloat16, 1e-2, 1.5e-1, 96),
+                                            (torch.float32, 1e-5, None, 40)])
+def test_block_cylinder_h128_vs_oracle(dtype, tf, tg, h):
+    """One GraphNetBlock on the CylinderFlow mesh vs the oracle. h = 96 and 40 are not kernel widths:
+    they run zero-padded to 128 / 64 (_engine.kernel_width; exact — same bounds as h = 128)."""
     from graphphysics.models.layers import GraphNetBlock
 
     n, ei = _cyl_graph()
-    h = 128
     torch.manual_seed(0)
     blk = GraphNetBlock(h)
     ref_p = {k: v.detach().clone().requires_grad_(True) for k, v in blk.named_parameters()}
@@ -247,6 +250,49 @@ def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
     if tg is None:
         assert relerr(y, yr) < tf
         assert relerr(y, y64) <= max(1e-6, 2 * relerr(yr, y64))
+        for k, p in m.named_parameters():
+            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, tie_tol=2e-3)
+        return
+    pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = O.encode_process_decode(x, ei, ea, pac, mp)
+    (yac.float() * gy).sum().backward()
+    assert relerr(y, y64) <= 2 * relerr(yac, y64)
+    for k, p in m.named_parameters():
+        assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
+
+
+@pytest.mark.parametrize("h,dtype", [(48, torch.float32), (48, torch.bfloat16), (100, torch.float32),
+                                     (100, torch.bfloat16)])
+def test_epd_any_hidden_size_vs_oracle(h, dtype):
+    """EncodeProcessDecode with hidden sizes the kernels are not instantiated for (the reference's
+    build_mlp takes any size: layers.py:77-113): zero-padded to the next kernel width (48 -> 64 on
+    the generic kernels, 100 -> 128 on the chained bf16 ones), with the RMSNorm over the true h.
+    Bounds as test_epd_cylinder_vs_oracle: fp32 output 1e-4 and gradients vs fp64 no worse than the
+    reference fp32 path; bf16 no further from fp64 than 2 x PyTorch's bf16 autocast."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    n, ei = _cyl_graph()
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(ei.shape[1], 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    mp = 3
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    rp = dict(ref.named_parameters())
+    yr = O.encode_process_decode(x, ei, ea, rp, mp)
+    (yr * gy).sum().backward()
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(x.double(), ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=dtype).to(DEV)
+    y = m(Data(x=x.to(DEV), edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+    (y * gy.to(DEV)).sum().backward()
+    if dtype == torch.float32:
+        assert relerr(y, yr) < 1e-4
         for k, p in m.named_parameters():
             assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, tie_tol=2e-3)
         return

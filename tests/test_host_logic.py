@@ -221,3 +221,34 @@ def test_load_checkpoint_updates_normalizer_buffers_in_place(tmp_path):
     for (s0, c0), na, nb in zip(before, a.normalizers(), b.normalizers()):
         assert nb._acc_sum is s0 and nb._acc_count is c0
         assert torch.equal(nb._acc_sum, na._acc_sum) and float(nb._acc_count) == 7.0
+
+
+@pytest.mark.parametrize("h", [48, 96, 100, 128])
+def test_padded_plan_layout_round_trips(h):
+    """Hidden sizes the kernels are not instantiated for run zero-padded to the next kernel width
+    (_engine.kernel_width): the padded parameter layout the kernels write gradients in must map
+    back onto the true layout exactly (ModelPlan.unpad), and the packed shapes cover the model."""
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(2, 11, 3, 2, h)
+    plan = m._get_plan()
+    W = _engine.kernel_width(h)
+    assert plan.padded == (W != h)
+    assert all(s.width == W for s in plan.specs)
+    if not plan.padded:
+        assert plan.numel_pad == plan.numel and plan.offsets_pad == plan.offsets
+        return
+    # a padded gradient buffer holding each true element at its padded position (and junk elsewhere)
+    true = torch.arange(plan.numel, dtype=torch.float32)
+    gp = torch.full((plan.numel_pad,), -1.0)
+    gp[plan._unpad_cpu] = true
+    assert torch.equal(plan.unpad(gp), true)
+    assert torch.unique(plan._unpad_cpu).numel() == plan.numel and int(plan._unpad_cpu.max()) < plan.numel_pad
+    blk = plan.specs[3]  # block 0's edge MLP: layer 0 = [e ‖ x_i ‖ x_j], three h-blocks each padded to W
+    assert blk.shapes[0][:2] == (W, 3 * W) and blk.shapes[0][4:] == (h, W)
+    dec = plan.specs[2]
+    assert dec.shapes[-1][:2] == (2, W) and dec.out_width == 2
+    with pytest.raises(ValueError, match="at most 128"):
+        _engine.kernel_width(144)

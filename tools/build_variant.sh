@@ -8,7 +8,9 @@ B=${SRC%.hip}
 mkdir -p $L/var
 EXTRA=""
 [ "$SRC" = "mgn_chain16.hip" ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable $EXTRA $2 -I include -c graph-physics_amd/csrc/$SRC -o $L/var/${B}_$1.o
+# SRCFILE=<path>: compile that file in place of graph-physics_amd/csrc/$SRC (e.g. a `git show HEAD:...` copy)
+IN=${SRCFILE:-graph-physics_amd/csrc/$SRC}
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable $EXTRA $2 -I include -I graph-physics_amd/csrc -c $IN -o $L/var/${B}_$1.o
 OBJS=""
 for s in mgn_mlp mgn_chain16 mgn_graph mgn_build mgn_prof; do
   if [ $s = $B ]; then OBJS="$OBJS $L/var/${B}_$1.o"; else OBJS="$OBJS $L/$s.o"; fi

@@ -8,6 +8,9 @@ for line in open(sys.argv[1], errors="replace"):
     p = line.split()
     if len(p) == 13 and p[0] in ("fwd16", "bwd16", "nfwd16", "nbwd16"):
         rows[p[0]].append([int(v) for v in p[1:]])
+stage = sorted(int(l.split()[1]) for l in open(sys.argv[1], errors="replace") if l.startswith("nfwd16_stage "))
+if stage:
+    print(f"nfwd16 staging (stager wave 4 of WG 0): median {stage[len(stage) // 2]} cycles over {len(stage)} launches")
 for name, rs in rows.items():
     med = [sorted(c)[len(c) // 2] for c in zip(*rs)]
     print(f"{name:7s} n={len(rs):3d} total={sum(med):6d}  " + " ".join(f"{v:6d}" for v in med))

@@ -2,7 +2,7 @@
 # run a short bench on the MGN_STAMPS variant library (tools/build_variant.sh stamps "-DMGN_STAMPS")
 L=graph-physics_amd/graphphysics/_lib
 cp $L/libmgn.so /tmp/libmgn_default.so
-cp $L/var/libmgn_stamps.so $L/libmgn.so
+cp $L/var/libmgn_${1:-stamps}.so $L/libmgn.so
 timeout -k 10 200 python3 bench.py --steps 3 --warmup 2 --cpu-steps 0 --no-mse --no-profile --no-secondary --sustain 0 > gpurun_out/stamps.log 2>&1
 rc=$?
 cp /tmp/libmgn_default.so $L/libmgn.so
