@@ -216,24 +216,28 @@ class _PackedWeights:
         self.pad_vec = None
         vec_slots = []
         if any(sp.padded for sp in plan.specs):
-            flat = plan.module._flat_params
-            f0 = flat.storage_offset()
-            idx = []
+            vecs, widths = [], []
             for sp in plan.specs:
-                if not sp.padded:
-                    continue
-                vecs = [lin.bias for lin in sp.linears] + ([sp.norm.scale] if sp.norm is not None else [])
-                widths = [s_[0] for s_ in sp.shapes] + ([sp.out_width] if sp.norm is not None else [])
-                for v, w in zip(vecs, widths):
-                    o = v.storage_offset() - f0
-                    vec_slots.append(len(idx))
-                    idx += [o + i if i < v.numel() else -1 for i in range(w)]
+                if sp.padded:
+                    vecs += [lin.bias for lin in sp.linears] + ([sp.norm.scale] if sp.norm is not None else [])
+                    widths += [s_[0] for s_ in sp.shapes] + ([sp.out_width] if sp.norm is not None else [])
+            # one gather from the parameters' common storage (flatten_parameters: always the case for
+            # a flattened model); otherwise (parameters in separate storages) a concatenation
+            st0 = vecs[0].untyped_storage()
+            self.flat = None
+            if all(v.untyped_storage().data_ptr() == st0.data_ptr() for v in vecs):
+                self.flat = torch.empty(0, dtype=torch.float32, device=device).set_(st0)
+            idx = []
+            for v, w in zip(vecs, widths):
+                vec_slots.append(len(idx))
+                o = v.storage_offset()
+                idx += [o + i if i < v.numel() else -1 for i in range(w)]
             pidx = torch.tensor(idx, dtype=torch.int64)
             self.pad_mask = (pidx >= 0).to(device=device, dtype=torch.float32)
             self.pad_idx = pidx.clamp(min=0).to(device)
             self.pad_vec = torch.zeros(len(idx), dtype=torch.float32, device=device)
             self.pad_tmp = torch.zeros_like(self.pad_vec)
-            self.flat = flat
+            self.vecs, self.widths = vecs, widths
         vbase = self.pad_vec.data_ptr() if self.pad_vec is not None else 0
         slot = iter(vec_slots)
         self.descs = []
@@ -265,8 +269,13 @@ class _PackedWeights:
     def repack(self, stream):
         nat.check(nat.lib().mgn_pack_weights(nat.ptr(self.jobs), self.njobs, self.max_el, stream))
         if self.pad_vec is not None:
-            torch.index_select(self.flat.detach(), 0, self.pad_idx, out=self.pad_tmp)
-            torch.mul(self.pad_tmp, self.pad_mask, out=self.pad_vec)
+            with torch.no_grad():
+                if self.flat is not None:
+                    torch.index_select(self.flat, 0, self.pad_idx, out=self.pad_tmp)
+                    torch.mul(self.pad_tmp, self.pad_mask, out=self.pad_vec)
+                else:
+                    torch.cat([torch.nn.functional.pad(v.detach().reshape(-1), (0, w - v.numel()))
+                               for v, w in zip(self.vecs, self.widths)], out=self.pad_vec)
 
 
 class ModelPlan:

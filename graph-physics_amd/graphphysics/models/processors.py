@@ -60,7 +60,9 @@ class EncodeProcessDecode(nn.Module):
         if self._plan is None:
             mlps = [] if self.only_processor else [self.nodes_encoder, self.edges_encoder,
                                                    self.decode_module]
-            kblocks = [0] * len(mlps)
+            # encoders read the raw features (columns not padded); the decoder reads the processor's
+            # (zero-padded) hidden state: one hidden-wide block, so its input gradient has the padded width
+            kblocks = [] if self.only_processor else [0, 0, 1]
             for blk in self.processor_list:
                 mlps += [blk.edge_block, blk.node_block]
                 kblocks += [3, 2]  # [e ‖ x_i ‖ x_j], [x ‖ aggr]: hidden-wide blocks

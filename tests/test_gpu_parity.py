@@ -152,10 +152,12 @@ def _cyl_graph():
 
 @pytest.mark.parametrize("dtype,tf,tg,h", [(torch.float32, 1e-5, None, 128), (torch.bfloat16, 1e-2, 1.5e-1, 128),
                                             (torch.float32, 1e-5, None, 96), (torch.bfloat16, 1e-2, 1.5e-1, 96),
-                                            (torch.float32, 1e-5, None, 40)])
+                                            (torch.float32, 1e-5, None, 24), (torch.float32, 1e-5, None, 36)])
 def test_block_cylinder_h128_vs_oracle(dtype, tf, tg, h):
-    """One GraphNetBlock on the CylinderFlow mesh vs the oracle. h = 96 and 40 are not kernel widths:
-    they run zero-padded to 128 / 64 (_engine.kernel_width; exact — same bounds as h = 128)."""
+    """One GraphNetBlock on the CylinderFlow mesh vs the oracle. h = 96, 36 and 24 are not kernel
+    widths: they run zero-padded to 128 / 64 / 32 (_engine.kernel_width; exact — same bounds as
+    h = 128). Sizes chosen without a ReLU tie on this input (no pre-activation within 1e-6 of its
+    layer's mean |z| in fp64; h = 40 has one at 8e-8, where any fp32 order may flip the unit)."""
     from graphphysics.models.layers import GraphNetBlock
 
     n, ei = _cyl_graph()
@@ -262,14 +264,16 @@ def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
         assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
 
 
-@pytest.mark.parametrize("h,dtype", [(48, torch.float32), (48, torch.bfloat16), (100, torch.float32),
-                                     (100, torch.bfloat16)])
+@pytest.mark.parametrize("h,dtype", [(36, torch.float32), (48, torch.float32), (48, torch.bfloat16),
+                                     (64, torch.bfloat16), (100, torch.float32), (100, torch.bfloat16)])
 def test_epd_any_hidden_size_vs_oracle(h, dtype):
     """EncodeProcessDecode with hidden sizes the kernels are not instantiated for (the reference's
     build_mlp takes any size: layers.py:77-113): zero-padded to the next kernel width (48 -> 64 on
     the generic kernels, 100 -> 128 on the chained bf16 ones), with the RMSNorm over the true h.
     Bounds as test_epd_cylinder_vs_oracle: fp32 output 1e-4 and gradients vs fp64 no worse than the
-    reference fp32 path; bf16 no further from fp64 than 2 x PyTorch's bf16 autocast."""
+    reference fp32 path; bf16 no further from fp64 than 2 x PyTorch's bf16 autocast (whole
+    gradient; 3 x per parameter). h = 64 (bf16) is the unpadded control on the same generic kernels
+    as h = 48."""
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils.data import Data
 
@@ -301,8 +305,16 @@ def test_epd_any_hidden_size_vs_oracle(h, dtype):
         yac = O.encode_process_decode(x, ei, ea, pac, mp)
     (yac.float() * gy).sum().backward()
     assert relerr(y, y64) <= 2 * relerr(yac, y64)
-    for k, p in m.named_parameters():
-        assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
+    # the whole gradient within 2 x autocast's error; each parameter within 3 x (a few small,
+    # partly dead-unit gradients sit near 2 x on the generic bf16 kernels for the unpadded h = 64
+    # control as well: measured 2.03 x, so the per-parameter ratio is noise, not padding)
+    names = [k for k, _ in m.named_parameters()]
+    cat = lambda d: torch.cat([d[k].reshape(-1).double().cpu() for k in names])  # noqa: E731
+    got = {k: p.grad for k, p in m.named_parameters()}
+    assert relerr(cat(got), cat({k: v.grad for k, v in p64.items()})) <= \
+        2 * relerr(cat({k: v.grad for k, v in pac.items()}), cat({k: v.grad for k, v in p64.items()}))
+    for k in names:
+        assert relerr(got[k], p64[k].grad) <= max(1e-2, 3 * relerr(pac[k].grad, p64[k].grad)), k
 
 
 @pytest.mark.parametrize("n,e", [(1100, 1000), (3000, 700)])

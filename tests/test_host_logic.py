@@ -250,5 +250,10 @@ def test_padded_plan_layout_round_trips(h):
     assert blk.shapes[0][:2] == (W, 3 * W) and blk.shapes[0][4:] == (h, W)
     dec = plan.specs[2]
     assert dec.shapes[-1][:2] == (2, W) and dec.out_width == 2
+    # the decoder reads the padded hidden state: its layer 0 (and so its input gradient, which the
+    # processor's last block reads W wide) is W wide
+    assert dec.shapes[0][:2] == (W, W) and dec.shapes[0][4:] == (h, W)
+    enc = plan.specs[0]  # the node encoder reads the raw 11 features: not padded
+    assert enc.shapes[0][:2] == (W, 11) and enc.out_width == W
     with pytest.raises(ValueError, match="at most 128"):
         _engine.kernel_width(144)

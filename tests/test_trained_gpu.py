@@ -138,8 +138,9 @@ def test_trained_one_step_mse_matches_reference(dtype):
     bf16: 2e-2), (2) end as one more draw from the reference's own run-to-run distribution:
     |MSE − mean of the reference runs| ≤ max(1e-5, 3 σ) per held-out frame, σ the runs' sample
     standard deviation (measured: runs 1.48–1.85e-4 / 2.92–3.56e-4, σ 1.5e-5 / 2.7e-5; libmgn fp32
-    1.34e-4 / 2.91e-4, bf16 1.51e-4 / 2.65e-4), and (3) train as well: loss curve medians within
-    10 % (fp32) / 20 % (bf16) of the first reference run."""
+    1.34e-4 / 2.91e-4, bf16 1.51e-4 / 2.65e-4), and (3) train as well: the median per-step
+    relative distance of the loss curve from the first reference run no larger than the other
+    reference runs' own (0.08–0.44: the curves decorrelate after ~5 steps, fp32 included)."""
     z = np.load(os.path.join(HERE, "cylinder_trained.npz"))
     zw = _weights_fixture()
     losses, mses, sim = _train(dtype, z)
@@ -154,7 +155,8 @@ def test_trained_one_step_mse_matches_reference(dtype):
           f"median {np.median(dl):.2e}, max {dl.max():.2e}")
     fp32 = dtype == torch.float32
     np.testing.assert_allclose(losses[:3], ref_losses[:3], rtol=1e-4 if fp32 else 2e-2)
-    assert np.median(dl) <= (0.1 if fp32 else 0.2)
+    ref_spread = max(np.median(np.abs(r - ref_losses) / np.abs(ref_losses)) for r in zw["chaos_losses"])
+    assert np.median(dl) <= ref_spread, (np.median(dl), ref_spread)
     bound = np.maximum(1e-5, 3.0 * sigma)
     assert np.all(np.abs(mses - center) <= bound), (mses, center, bound)
     # normaliser accumulators after 300 training forwards: the same statistics (the means — the
