@@ -36,6 +36,10 @@
 #define MGN_PROJ_HANDOFF 1  // A/B builds: 0 = the tile wave computes the next block's projections itself
 #endif
 
+#ifndef MGN_BWD_HANDOFF
+#define MGN_BWD_HANDOFF 1  // A/B builds: 0 = the node backward's tile wave computes d_aggr itself
+#endif
+
 #ifndef MGN_NODE_AG
 #define MGN_NODE_AG 6  // in-edges gathered per round trip by the node-MLP aggregation (8 spills)
 #endif
@@ -56,6 +60,10 @@ constexpr size_t LDS_V = (size_t)6 * H * 4;             // 4 bias vectors + scal
 constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose scratch
 constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
 constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
+// node backward hand-off: k-steps 0-1 of each tile wave's dZ0 operand (2 KiB per wave; k-steps 2-3
+// go through the partner's scratch)
+constexpr size_t LDS_HAND = (size_t)(NW / 2) * 64 * 2 * 16;
+static_assert(LDS_TOTAL + LDS_HAND <= 163840, "node backward hand-off exceeds 160 KiB of LDS");
 // edge kernels, per waves-per-workgroup NWK (8: two waves per SIMD; 12: three): forward = weights |
 // bias[4] + scale | scratch, backward = weights | scale | scratch | dscale partials (12 waves: 160 KiB)
 constexpr size_t LDS_VF = (size_t)5 * H * 4, LDS_VB = (size_t)H * 4;
@@ -1062,6 +1070,33 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     STAMP_PRINT("nfwd16");
 }
 
+// d_aggr = dZ0·W0aᵀ of node tile `tile` by the partner wave of the tile wave that computed dZ0
+// (chain16_node_bwd_kernel's hand-off): the 32 weight fragments (global, L2) are loaded BEFORE
+// waiting, so their round trips run under the tile wave's layers 3..1 instead of after them; then
+// dZ0's operand comes from LDS (h0: k-steps 0-1, h1 = this wave's scratch: k-steps 2-3). Same
+// fragments, same k order as the tile wave's own loop: d_aggr is bit-identical.
+__device__ __forceinline__ void node_aggr_partner(const ChainNodeBwdArgs& a, int64_t tile, unsigned* flag,
+                                                  const bf16x8* h0, __bf16* scr, int lane) {
+    const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
+    const int vo = gfrag_voff(lane);
+    bf16x8 fr[4][8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) fr[s][t] = gfrag(rs, vo, (8 + t) * 4 + s);
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
+    const bf16x8* h1 = reinterpret_cast<const bf16x8*>(scr);
+    const bf16x8 B[4] = {h0[2 * lane], h0[2 * lane + 1], h1[2 * lane], h1[2 * lane + 1]};
+    f4 acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[s][t], B[s], acc[t]);
+    store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // (the LDS reads of h1 precede its reuse)
+}
+
 // DIN2: dx_out in the pair layout (written by the next block's node_grad)
 template <bool DIN2>
 __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdArgs a) {
@@ -1128,11 +1163,17 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     // as the node forward: with at most one tile per first-half wave, the second half stages the
     // weights while the first half runs phase A
     const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
+    // d_aggr hand-off (split launches): the partner w + NW/2 of tile wave w, idle after the staging,
+    // computes the tile's aggregate-half gradient (global weight fragments) once w has put dZ0 in LDS
+    const bool handoff = MGN_BWD_HANDOFF && split;
+    unsigned* flags = reinterpret_cast<unsigned*>(vec + H);  // [NW/2], in the vector region's spare
+    bf16x8* hand = reinterpret_cast<bf16x8*>(smem + LDS_TOTAL);  // [NW/2][64 lanes][2]
     f4 acc[8];
     u32x2 d[8];
     unsigned mk[3];
     STAMP_DECL;
     if (split) {
+        if (threadIdx.x < NW / 2) flags[threadIdx.x] = 0u;
         if (wave >= NW / 2)
             stage16<4, NW / 2 * 64>(W, a.wtpack, a.woff, a.wks, true, threadIdx.x - NW / 2 * 64);
         else if (tile < a.ntiles)
@@ -1140,8 +1181,15 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     } else {
         stage16(W, a.wtpack, a.woff, a.wks, true);
     }
+    STAMP(7);  // wave 0: its phase A (split launches)
     __syncthreads();
     STAMP(0);
+    if (handoff && wave >= NW / 2) {
+        const int pw = wave - NW / 2;
+        const int64_t pt = (int64_t)pw * gridDim.x + blockIdx.x;  // the partner's (only) tile
+        if (pt < a.ntiles) node_aggr_partner(a, pt, flags + pw, hand + pw * 128, scr, lane);
+        tile = a.ntiles;  // no tile loop; the workgroup's dscale reduction below still needs this wave
+    }
     for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
         if (!split || tile != first) phase_a(tile, acc, d, mk);
         STAMP(1);
@@ -1154,11 +1202,24 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             relu_mask(acc, mk[l - 1]);
             to_operand(acc, B);
         }
+        STAMP(3);
+        if (handoff) {  // dZ0's operand to the partner: k-steps 0-1 via the hand region, 2-3 via its scratch
+            bf16x8* h0 = hand + wave * 128;
+            bf16x8* h1 = reinterpret_cast<bf16x8*>(scr + (NW / 2) * SROWS * SLD);
+            h0[2 * lane] = B[0];
+            h0[2 * lane + 1] = B[1];
+            h1[2 * lane] = B[2];
+            h1[2 * lane + 1] = B[3];
+            if (lane == 0) __hip_atomic_store(flags + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
         gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, nullptr}, tile, a.M);
+        STAMP(4);
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
         store_rows(acc, scr, a.dx_part, tile, a.M, lane);
+        STAMP(5);
+        if (handoff) continue;  // (one tile per wave: the loop ends)
         {
             const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
             const int vo = gfrag_voff(lane);
@@ -1173,6 +1234,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
                 for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[t], B[s], acc[t]);
             }
         }
+        STAMP(6);
         store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // gathered by the chained edge backward
         STAMP(2);
     }
@@ -1687,11 +1749,11 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = 0;
     if (M == 0) return 0;
     const auto kern = din2 ? chain16_node_bwd_kernel<true> : chain16_node_bwd_kernel<false>;
-    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
+    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL + LDS_HAND)) return e2;
     const int grid = chain16_node_backward_parts(M);
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL + LDS_HAND, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }

@@ -28,6 +28,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "graph-physics_amd")]
 HBM_PEAK = 8000.0
+MFMA_PEAK_BF16 = 2500.0  # TFLOP/s, dense bf16 (MI355X_MICROARCH.md)
 
 
 def timed(fn, reps, sync=True):
@@ -82,15 +83,21 @@ def rollout_row(a, dev):
     nat.profile_enable(False)
     n, e, h = frames[0].x.shape[0], frames[0].edge_index.shape[1], 128
     kern = {k: {"avg_us": round(1000 * ms / c, 2), "launches": c} for k, (ms, c) in prof.items() if c}
-    # inference edge kernel, compulsory bytes per edge: e in, e' out, z out (bf16) + rden + fp32 P_i/P_j
-    eb = e * (3 * 2 * h + 4 + 2 * 4 * h)
+    # MLP kernels on the MFMA roof. The inference edge kernel runs 8h² FLOPs per edge
+    # (layer 0's e block + three h x h Linears; the x blocks are the node projections); one rollout
+    # step is one forward F_fwd = MP (12h²E + 10h²N) + encoders + decoder
     fe = kern.get("fwd_edge")
     roof = None
+    f_fwd = 15 * (12 * h * h * e + 10 * h * h * n) + 2 * (3 * h + 3 * h * h) * e + 2 * (11 * h + 3 * h * h) * n \
+        + 2 * (3 * h * h + 2 * h) * n
     if fe:
-        gbs = eb / (fe["avg_us"] * 1e-6) / 1e9
-        roof = {"kernel": "fwd_edge (inference)", "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK,
-                "unit": "GB/s", "frac": round(gbs / HBM_PEAK, 4), "bytes_per_launch": eb,
-                "avg_launch_us": fe["avg_us"]}
+        fl = 8 * h * h * e
+        tf = fl / (fe["avg_us"] * 1e-6) / 1e12
+        roof = {"kernel": "fwd_edge (inference)", "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_PEAK_BF16,
+                "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_BF16, 4), "flops_per_launch": fl,
+                "avg_launch_us": fe["avg_us"],
+                # the same kernel's compulsory bytes (e in, e' / z out bf16, rden, fp32 P_i/P_j gathers)
+                "hbm_gbs": round(e * (3 * 2 * h + 4 + 2 * 4 * h) / (fe["avg_us"] * 1e-6) / 1e9, 1)}
     # CPU baseline: the oracle's eval forward on the same batch (reference ops, fp32)
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
@@ -102,13 +109,17 @@ def rollout_row(a, dev):
     x, y, ei, ea = (f0.x.cpu(), f0.y.cpu(), f0.edge_index.cpu(), f0.edge_attr.cpu())
     with torch.no_grad():
         osim.forward(x, y, ei, ea, training=True)
-        t_cpu, _ = timed(lambda: osim.forward(x, y, ei, ea, training=False), 2, sync=False)
+        t_cpu, _ = timed(lambda: osim.forward(x, y, ei, ea, training=False), a.cpu_forwards, sync=False)
+    step_tf = f_fwd * a.steps / dt / 1e12
     return {"value": round(a.steps / dt, 2), "unit": "rollout steps/s", "ms_per_step": round(1000 * dt / a.steps, 3),
+            "step_mfma": {"flops_per_step": f_fwd, "tflops_per_s": round(step_tf, 2),
+                          "frac": round(step_tf / MFMA_PEAK_BF16, 4), "note": "F_fwd (SURVEY §8d) / measured ms_per_step"},
             "steps": a.steps, "config": {"workload": "Cfg B rollout: 8 CylinderFlow graphs, MP=15, h=128, bf16",
                                          "nodes": n, "edges": e},
             "execution": "hipGraph replay per step (inference block kernels)", "roofline": roof, "kernels": kern,
             "cpu_baseline": {"value": round(1.0 / t_cpu, 4), "unit": "rollout steps/s", "cores": cores,
-                             "kind": "port", "sample": "2 timed eval forwards of the same batch (oracle, fp32)"}}
+                             "kind": "port", "sample": "%d timed eval forwards (median) of the same batch "
+                                                       "after one warm-up (oracle, fp32)" % a.cpu_forwards}}
 
 
 def graph_row(dev):
@@ -176,6 +187,7 @@ def world_row(dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--cpu-forwards", type=int, default=10, help="timed CPU (oracle) eval forwards")
     a = ap.parse_args()
     import __graft_entry__ as ge
 
