@@ -92,7 +92,9 @@ def make_workload(a, dev, rank, mesh):
                     edge_index=torch.from_numpy(b["edge_index"]).to(dev),
                     edge_attr=torch.from_numpy(b["edge_attr"]).to(dev), pos=torch.from_numpy(b["pos"]).to(dev))
         return b, data, dict(node_in=11, edge_in=3, out=2, fs=(0, 2), os=(0, 2), nti=2), \
-            "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (Cfg B)" % (a.mp, a.hidden, a.batch), \
+            "CylinderFlow MGN %dMP h=%d, batch=%d graphs per GPU (%s)" % (
+                a.mp, a.hidden, a.batch, "Cfg B" if (a.mp, a.hidden, a.batch) == (15, 128, 8) else
+                "Cfg A" if (a.mp, a.hidden, a.batch) == (5, 32, 1) else "custom"), \
             "%d jittered copies of the reference in-tree CylinderFlow mesh per GPU" % a.batch
     if a.workload == "plate":
         g, lay = meshes.plate_graph(dev, seed=rank)
