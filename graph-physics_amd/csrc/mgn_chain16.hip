@@ -60,10 +60,7 @@ constexpr size_t LDS_V = (size_t)6 * H * 4;             // 4 bias vectors + scal
 constexpr size_t LDS_S = (size_t)NW * SROWS * SLD * 2;  // per-wave transpose scratch
 constexpr size_t LDS_R = (size_t)NW * H * 4;            // backward: per-wave dscale partials
 constexpr size_t LDS_TOTAL = LDS_W + LDS_V + LDS_S + LDS_R;
-// node backward hand-off: k-steps 0-1 of each tile wave's dZ0 operand (2 KiB per wave; k-steps 2-3
-// go through the partner's scratch)
-constexpr size_t LDS_HAND = (size_t)(NW / 2) * 64 * 2 * 16;
-static_assert(LDS_TOTAL + LDS_HAND <= 163840, "node backward hand-off exceeds 160 KiB of LDS");
+
 // edge kernels, per waves-per-workgroup NWK (8: two waves per SIMD; 12: three): forward = weights |
 // bias[4] + scale | scratch, backward = weights | scale | scratch | dscale partials (12 waves: 160 KiB)
 constexpr size_t LDS_VF = (size_t)5 * H * 4, LDS_VB = (size_t)H * 4;
@@ -1070,13 +1067,16 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     STAMP_PRINT("nfwd16");
 }
 
-// d_aggr = dZ0·W0aᵀ of node tile `tile` by the partner wave of the tile wave that computed dZ0
-// (chain16_node_bwd_kernel's hand-off): the 32 weight fragments (global, L2) are loaded BEFORE
-// waiting, so their round trips run under the tile wave's layers 3..1 instead of after them; then
-// dZ0's operand comes from LDS (h0: k-steps 0-1, h1 = this wave's scratch: k-steps 2-3). Same
-// fragments, same k order as the tile wave's own loop: d_aggr is bit-identical.
-__device__ __forceinline__ void node_aggr_partner(const ChainNodeBwdArgs& a, int64_t tile, unsigned* flag,
-                                                  const bf16x8* h0, __bf16* scr, int lane) {
+// Layer 0 of node tile `tile`'s backward by the partner wave of the tile wave that ran layers 3..1
+// (chain16_node_bwd_kernel's hand-off): the aggregate block's 32 weight fragments (global, L2) and
+// the tile's dx_out rows are loaded BEFORE waiting, so their round trips run under the tile wave's
+// layers; then dZ0's operand comes from LDS (k-steps 0-1 from the tile wave's scratch, 2-3 from this
+// wave's own) and the partner runs what the tile wave would have: d_aggr = dZ0·W0aᵀ, the dZ0 save and
+// dx_part = dx_out + dZ0·W0xᵀ (LDS image). Each output's operations in the same order: bit-identical.
+template <bool DIN2>
+__device__ __forceinline__ void node_layer0_partner(const ChainNodeBwdArgs& a, int64_t tile, unsigned* flag,
+                                                    const __bf16* W, __bf16* tscr, __bf16* scr, int lane) {
+    const int g = lane >> 4;
     const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
     const int vo = gfrag_voff(lane);
     bf16x8 fr[4][8];
@@ -1084,9 +1084,14 @@ __device__ __forceinline__ void node_aggr_partner(const ChainNodeBwdArgs& a, int
     for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < 8; ++t) fr[s][t] = gfrag(rs, vo, (8 + t) * 4 + s);
+    u32x2 d[8];
+    load_acc_row<DIN2>(d, a.dout + clamp_row(tile * TR + (lane & 15), a.M) * H, g);
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
+    const bf16x8* h0 = reinterpret_cast<const bf16x8*>(tscr);
     const bf16x8* h1 = reinterpret_cast<const bf16x8*>(scr);
     const bf16x8 B[4] = {h0[2 * lane], h0[2 * lane + 1], h1[2 * lane], h1[2 * lane + 1]};
+    lds_fence();  // (own scratch reads back before the stores below reuse it)
+    // the aggregate half first: its fragments' registers are free again for the LDS half
     f4 acc[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1094,7 +1099,11 @@ __device__ __forceinline__ void node_aggr_partner(const ChainNodeBwdArgs& a, int
     for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[s][t], B[s], acc[t]);
-    store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // (the LDS reads of h1 precede its reuse)
+    store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // gathered by the chained edge backward
+    gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, nullptr}, tile, a.M);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
+    store_rows(acc, scr, a.dx_part, tile, a.M, lane);
 }
 
 // DIN2: dx_out in the pair layout (written by the next block's node_grad)
@@ -1163,11 +1172,11 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     // as the node forward: with at most one tile per first-half wave, the second half stages the
     // weights while the first half runs phase A
     const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
-    // d_aggr hand-off (split launches): the partner w + NW/2 of tile wave w, idle after the staging,
-    // computes the tile's aggregate-half gradient (global weight fragments) once w has put dZ0 in LDS
+    // layer-0 hand-off (split launches): the partner w + NW/2 of tile wave w, idle after the staging,
+    // runs the tile's layer 0 (its aggregate half from global weight fragments) once w has put dZ0's
+    // operand in LDS (w's scratch and the partner's: no extra LDS)
     const bool handoff = MGN_BWD_HANDOFF && split;
     unsigned* flags = reinterpret_cast<unsigned*>(vec + H);  // [NW/2], in the vector region's spare
-    bf16x8* hand = reinterpret_cast<bf16x8*>(smem + LDS_TOTAL);  // [NW/2][64 lanes][2]
     f4 acc[8];
     u32x2 d[8];
     unsigned mk[3];
@@ -1187,7 +1196,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     if (handoff && wave >= NW / 2) {
         const int pw = wave - NW / 2;
         const int64_t pt = (int64_t)pw * gridDim.x + blockIdx.x;  // the partner's (only) tile
-        if (pt < a.ntiles) node_aggr_partner(a, pt, flags + pw, hand + pw * 128, scr, lane);
+        if (pt < a.ntiles) node_layer0_partner<DIN2>(a, pt, flags + pw, W, scr - (NW / 2) * SROWS * SLD, scr, lane);
         tile = a.ntiles;  // no tile loop; the workgroup's dscale reduction below still needs this wave
     }
     for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
@@ -1203,14 +1212,15 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             to_operand(acc, B);
         }
         STAMP(3);
-        if (handoff) {  // dZ0's operand to the partner: k-steps 0-1 via the hand region, 2-3 via its scratch
-            bf16x8* h0 = hand + wave * 128;
+        if (handoff) {  // dZ0's operand to the partner (k-steps 0-1: this scratch, 2-3: the partner's)
+            bf16x8* h0 = reinterpret_cast<bf16x8*>(scr);
             bf16x8* h1 = reinterpret_cast<bf16x8*>(scr + (NW / 2) * SROWS * SLD);
             h0[2 * lane] = B[0];
             h0[2 * lane + 1] = B[1];
             h1[2 * lane] = B[2];
             h1[2 * lane + 1] = B[3];
             if (lane == 0) __hip_atomic_store(flags + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            continue;  // (one tile per wave: the loop ends)
         }
         // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
         gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, nullptr}, tile, a.M);
@@ -1219,7 +1229,6 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
         store_rows(acc, scr, a.dx_part, tile, a.M, lane);
         STAMP(5);
-        if (handoff) continue;  // (one tile per wave: the loop ends)
         {
             const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
             const int vo = gfrag_voff(lane);
@@ -1749,11 +1758,11 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     *nparts = 0;
     if (M == 0) return 0;
     const auto kern = din2 ? chain16_node_bwd_kernel<true> : chain16_node_bwd_kernel<false>;
-    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL + LDS_HAND)) return e2;
+    if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
     const int grid = chain16_node_backward_parts(M);
     *nparts = grid;
     ProfScope ps(PROF_BWD_NODE, st);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL + LDS_HAND, st, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
 }
