@@ -1067,16 +1067,46 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     STAMP_PRINT("nfwd16");
 }
 
-// Layer 0 of node tile `tile`'s backward by the partner wave of the tile wave that ran layers 3..1
-// (chain16_node_bwd_kernel's hand-off): the aggregate block's 32 weight fragments (global, L2) and
-// the tile's dx_out rows are loaded BEFORE waiting, so their round trips run under the tile wave's
-// layers; then dZ0's operand comes from LDS (k-steps 0-1 from the tile wave's scratch, 2-3 from this
-// wave's own) and the partner runs what the tile wave would have: d_aggr = dZ0·W0aᵀ, the dZ0 save and
-// dx_part = dx_out + dZ0·W0xᵀ (LDS image). Each output's operations in the same order: bit-identical.
-template <bool DIN2>
-__device__ __forceinline__ void node_layer0_partner(const ChainNodeBwdArgs& a, int64_t tile, unsigned* flag,
-                                                    const __bf16* W, __bf16* tscr, __bf16* scr, int lane) {
-    const int g = lane >> 4;
+// The wave's bf16 B operand (a 16-row tile, k-steps 0..3) as R8 octets 2*tile, 2*tile+1 of dst, through
+// the wave's scratch (the store path of gemm16_st without its GEMM)
+__device__ __forceinline__ void store_operand_r8(const bf16x8 (&B)[4], __bf16* scr, __bf16* dst, int64_t tile,
+                                                 int lane) {
+    const int m = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        if ((m >> 3) == u) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const u32x4 b = __builtin_bit_cast(u32x4, B[t >> 1]);
+                const u32x2 w = (t & 1) ? u32x2{b[2], b[3]} : u32x2{b[0], b[1]};
+                *reinterpret_cast<u32x2*>(scr + (m & 7) * SLD + 16 * t + 4 * g) = w;
+            }
+        }
+        lds_fence();
+        u32x2 rv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rv[q][0] = *reinterpret_cast<const unsigned*>(scr + q * SLD + 2 * lane);
+        bf16x8 c0, c1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bf16x2 p = __builtin_bit_cast(bf16x2, rv[q][0]);
+            c0[q] = p[0];
+            c1[q] = p[1];
+        }
+        __bf16* p = dst + (((int64_t)tile * 2 + u) * H + 2 * lane) * 8;
+        *reinterpret_cast<bf16x8*>(p) = c0;
+        *reinterpret_cast<bf16x8*>(p + 8) = c1;
+        lds_fence();
+    }
+}
+
+// The aggregate half of node tile `tile`'s layer-0 backward, d_aggr = dZ0·W0aᵀ, and the dZ0 save, by the
+// partner wave of the tile wave that ran layers 3..1 (chain16_node_bwd_kernel's hand-off; the tile wave
+// keeps the LDS half, dx_part): the 32 weight fragments (global, L2) are loaded BEFORE waiting, so their
+// round trips run under the tile wave's layers; then dZ0's operand comes from LDS (k-steps 0-1 from the
+// tile wave's scratch, 2-3 from this wave's own). Same operations in the same order: bit-identical.
+__device__ __forceinline__ void node_aggr_partner(const ChainNodeBwdArgs& a, int64_t tile, unsigned* flag,
+                                                  const __bf16* tscr, __bf16* scr, int lane) {
     const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.wtpack + a.woff[0]);
     const int vo = gfrag_voff(lane);
     bf16x8 fr[4][8];
@@ -1084,14 +1114,11 @@ __device__ __forceinline__ void node_layer0_partner(const ChainNodeBwdArgs& a, i
     for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < 8; ++t) fr[s][t] = gfrag(rs, vo, (8 + t) * 4 + s);
-    u32x2 d[8];
-    load_acc_row<DIN2>(d, a.dout + clamp_row(tile * TR + (lane & 15), a.M) * H, g);
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
     const bf16x8* h0 = reinterpret_cast<const bf16x8*>(tscr);
     const bf16x8* h1 = reinterpret_cast<const bf16x8*>(scr);
     const bf16x8 B[4] = {h0[2 * lane], h0[2 * lane + 1], h1[2 * lane], h1[2 * lane + 1]};
     lds_fence();  // (own scratch reads back before the stores below reuse it)
-    // the aggregate half first: its fragments' registers are free again for the LDS half
     f4 acc[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1100,10 +1127,7 @@ __device__ __forceinline__ void node_layer0_partner(const ChainNodeBwdArgs& a, i
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = mfma16(fr[s][t], B[s], acc[t]);
     store_rows<true>(acc, scr, a.d_aggr, tile, a.M, lane);  // gathered by the chained edge backward
-    gemm16_st(acc, W, 0, B, lane, scr, StoreDst{a.dz8, nullptr}, tile, a.M);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] += bf4(d[t]);
-    store_rows(acc, scr, a.dx_part, tile, a.M, lane);
+    store_operand_r8(B, scr, a.dz8, tile, lane);            // dZ0 (R8): the weight-gradient ring's operand
 }
 
 // DIN2: dx_out in the pair layout (written by the next block's node_grad)
@@ -1173,8 +1197,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     // weights while the first half runs phase A
     const bool split = a.ntiles <= (int64_t)gridDim.x * (NW / 2);
     // layer-0 hand-off (split launches): the partner w + NW/2 of tile wave w, idle after the staging,
-    // runs the tile's layer 0 (its aggregate half from global weight fragments) once w has put dZ0's
-    // operand in LDS (w's scratch and the partner's: no extra LDS)
+    // runs the aggregate half of the tile's layer 0 (global weight fragments) and the dZ0 save once w
+    // has put dZ0's operand in LDS (w's scratch and the partner's: no extra LDS); w keeps the LDS half
     const bool handoff = MGN_BWD_HANDOFF && split;
     unsigned* flags = reinterpret_cast<unsigned*>(vec + H);  // [NW/2], in the vector region's spare
     f4 acc[8];
@@ -1196,7 +1220,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     if (handoff && wave >= NW / 2) {
         const int pw = wave - NW / 2;
         const int64_t pt = (int64_t)pw * gridDim.x + blockIdx.x;  // the partner's (only) tile
-        if (pt < a.ntiles) node_layer0_partner<DIN2>(a, pt, flags + pw, W, scr - (NW / 2) * SROWS * SLD, scr, lane);
+        if (pt < a.ntiles) node_aggr_partner(a, pt, flags + pw, scr - (NW / 2) * SROWS * SLD, scr, lane);
         tile = a.ntiles;  // no tile loop; the workgroup's dscale reduction below still needs this wave
     }
     for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
@@ -1220,6 +1244,19 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
             h1[2 * lane] = B[2];
             h1[2 * lane + 1] = B[3];
             if (lane == 0) __hip_atomic_store(flags + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // the LDS half: dx_part = dx_out + dZ0·W0xᵀ, stored straight from the accumulator layout
+            // (the scratch now belongs to the partner; the partner writes the dZ0 save)
+            gemm16(acc, W, 0, B, lane);
+            const int64_t row = tile * TR + m;
+            if (row < a.M) {
+                __bf16* p = a.dx_part + row * H;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const f4 v = acc[t] + bf4(d[t]);
+                    *reinterpret_cast<bf16x4*>(p + 16 * t + 4 * g) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2],
+                                                                            (__bf16)v[3]};
+                }
+            }
             continue;  // (one tile per wave: the loop ends)
         }
         // layer 0: dx_part = dx_out + dZ0·W0x (LDS image), d_aggr = dZ0·W0a (global fragments)
