@@ -432,6 +432,11 @@ def main():
                                          mp=15, hidden=128, batch=8)
         sec["cfgA"] = secondary(a, dev, mesh, "Config A: training_config/cylinder.json (MP=5, h=32, fp32, B=1)",
                                 cpu_steps=(20 if a.cpu_steps > 0 else 0), dtype="fp32", mp=5, hidden=32, batch=1)
+        # BASELINE config 2 at training_config/plate.json's sizes (MP=10, h=64; the reference file
+        # selects its transformer processor, out of scope: this is the MGN processor at those sizes)
+        sec["cfgC_plate"] = secondary(a, dev, mesh, "Config C: DeformingPlate MGN at plate.json's sizes (MP=10, h=64, "
+                                      "bf16), world edges + relative-position features, 1 graph",
+                                      dtype="bf16", mp=10, hidden=64, batch=1, workload="plate")
         out["secondary"] = sec
     print(json.dumps(out), flush=True)
     if world > 1:

@@ -1098,6 +1098,12 @@ struct RgArgs {
     RgJob job[12];
 };
 
+// fp32 ring (wgrad_ring_f32_kernel) for fp32 h=128 MLPs (A/B builds: 0 = the generic weight-gradient
+// kernel, 3 launches + 2 reductions per block)
+#ifndef MGN_RING_F32
+#define MGN_RING_F32 1
+#endif
+
 // A-B builds only: cache policy of the ring's LDS-DMA streams (bit 0: X operand nt, bit 1: dZ nt)
 #ifndef MGN_RING_NT
 #define MGN_RING_NT 0
@@ -1109,6 +1115,49 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 }
 
 __device__ __forceinline__ int rg_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// Slab write of a ring workgroup: the waves' 2x4 accumulator tiles (wave (wn, wk): feature blocks
+// 2wn + i, column blocks 4wk + j of the job's 128-column block) through a canonical LDS tile (row pitch
+// H+4 floats) + the bias row, then coalesced slab stores (as mlp_wgrad_kernel). smem must be free.
+__device__ __forceinline__ void ring_epilogue(const RgJob& job, int chunk, const f4 (&acc)[2][4], const float (&bsum)[2],
+                                              bool do_bias, int wn, int wk, int lane, char* smem) {
+    constexpr int H = 128;
+    constexpr int LP = H + 4;
+    float* tile = reinterpret_cast<float*>(smem);
+    float* btile = tile + H * LP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                tile[((2 * wn + i) * 16 + (lane >> 4) * 4 + r) * LP + (4 * wk + j) * 16 + (lane & 15)] = acc[i][j][r];
+        float t = bsum[i];
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        if (do_bias && lane < 16) btile[(2 * wn + i) * 16 + lane] = t;
+    }
+    __syncthreads();
+    float* part = job.part + (int64_t)chunk * job.G;
+    constexpr int C4 = H / 4;
+    const int col0 = job.col0;
+    const bool vec = ((job.G | job.w_off | (int64_t)job.k) & 3) == 0;
+    for (int it = threadIdx.x; it < H * C4; it += 512) {
+        const int n = it / C4, k4 = (it % C4) * 4;
+        const int kc = col0 + k4;
+        if (n >= job.n || kc >= job.k) continue;
+        const f4 v = *reinterpret_cast<const f4*>(tile + n * LP + k4);
+        float* dst = part + job.w_off + (int64_t)n * job.k + kc;
+        if (vec && kc + 4 <= job.k) {
+            *reinterpret_cast<f4*>(dst) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (kc + e < job.k) dst[e] = v[e];
+        }
+    }
+    if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
+}
 
 __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
     constexpr int H = 128;
@@ -1248,41 +1297,109 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (unconsumed) ring loads
     __syncthreads();
-    // canonical tile (row pitch H+4 floats) + bias row, then coalesced slab stores (as mlp_wgrad_kernel)
-    constexpr int LP = H + 4;
-    float* tile = reinterpret_cast<float*>(smem);
-    float* btile = tile + H * LP;
+    ring_epilogue(job, chunk, acc, bsum, do_bias, wn, wk, lane, smem);
+}
+
+// fp32 form of the ring (the reference's dtype, h = 128): the same self-contained jobs and slabs, on
+// v_mfma_f32_16x16x4_f32. A 32-row stage is 16 KiB per operand (R8 dZ: the stage's 4 octets are
+// contiguous; X: R8 octets, or 32 plain rows for the re-gathered layer-0 inputs) — 4 ring slots of
+// 32 KiB, 3 stages in flight; every wave issues 4 pieces of 1 KiB per stage. The reduction over the
+// stage's rows runs in octet order: MFMA j (0..7) takes row 8g + j into k-lane g, so lane (c, g) reads
+// its 8 values of one R8 column with two 16-byte LDS loads (dZ, and X when R8).
+constexpr int RF_RS = 32;
+constexpr int RF_NS = 4;
+constexpr int RF_SLOT = 2 * RF_RS * 128 * 4;
+constexpr size_t RF_LDS = (size_t)RF_NS * RF_SLOT;
+static_assert(RF_LDS >= (size_t)128 * 132 * 4 + 512, "the slab epilogue's tile reuses the ring");
+
+__global__ __launch_bounds__(512) void wgrad_ring_f32_kernel(RgArgs a) {
+    constexpr int H = 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wn = w & 3, wk = w >> 2;
+    int jn = 0;
+    while (jn + 1 < a.njobs && (int)blockIdx.x >= a.job[jn + 1].wg0) ++jn;
+    const RgJob job = a.job[jn];
+    const int chunk = (int)blockIdx.x - job.wg0;
+    const int64_t r_begin = (int64_t)chunk * job.rows_per_chunk;
+    const int64_t r_end = r_begin + job.rows_per_chunk < job.RP ? r_begin + job.rows_per_chunk : job.RP;
+    const int nst = r_end > r_begin ? (int)((r_end - r_begin) / RF_RS) : 0;  // 0: zero slab
+    const bool staged = job.ld != 0;
+    const float* Z = reinterpret_cast<const float*>(job.z);
+    const float* X = reinterpret_cast<const float*>(job.x);
+    auto issue = [&](int s) {
+        const int sc = s < nst ? s : nst - 1;  // past the end: reload the last stage, never consumed
+        const int64_t m0 = r_begin + (int64_t)sc * RF_RS;
+        char* slot = smem + (s % RF_NS) * RF_SLOT;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+        for (int p = 0; p < 2; ++p) {
+            const int pc = 2 * w + p;  // piece 0..15 of each operand
+            glds16(Z + m0 * H + pc * 256 + lane * 4, slot + pc * 1024);
+            const float* xs;
+            if (!staged) {
+                xs = X + ((((m0 >> 3) + (pc >> 2)) * job.kp) + (pc & 3) * 32) * 8 + lane * 4;
+            } else {
+                const int64_t r = m0 + 2 * pc + (lane >> 5);
+                xs = X + (r < job.M ? r : job.M - 1) * job.ld + (lane & 31) * 4;
+            }
+            glds16(xs, slot + RF_SLOT / 2 + pc * 1024);
+        }
+    };
+    f4 acc[2][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                tile[((2 * wn + i) * 16 + (lane >> 4) * 4 + r) * LP + (4 * wk + j) * 16 + (lane & 15)] = acc[i][j][r];
-        float t = bsum[i];
-        t += __shfl_xor(t, 16);
-        t += __shfl_xor(t, 32);
-        if (do_bias && lane < 16) btile[(2 * wn + i) * 16 + lane] = t;
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float bsum[2] = {0.f, 0.f};
+    const bool do_bias = job.b_off >= 0 && wk == 0;
+    const int c16 = lane & 15, g = lane >> 4;
+    if (nst > 0) {
+#pragma unroll
+        for (int p = 0; p < RF_NS - 1; ++p) issue(p);
     }
-    __syncthreads();
-    float* part = job.part + (int64_t)chunk * job.G;
-    constexpr int C4 = H / 4;
-    const bool vec = ((job.G | job.w_off | (int64_t)job.k) & 3) == 0;
-    for (int it = threadIdx.x; it < H * C4; it += 512) {
-        const int n = it / C4, k4 = (it % C4) * 4;
-        const int kc = col0 + k4;
-        if (n >= job.n || kc >= job.k) continue;
-        const f4 v = *reinterpret_cast<const f4*>(tile + n * LP + k4);
-        float* dst = part + job.w_off + (int64_t)n * job.k + kc;
-        if (vec && kc + 4 <= job.k) {
-            *reinterpret_cast<f4*>(dst) = v;
-        } else {
+    for (int s = 0; s < nst; ++s) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (RF_NS - 2)) : "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(s + RF_NS - 1);
+        const float* zi = reinterpret_cast<const float*>(smem + (s % RF_NS) * RF_SLOT);
+        const float* xi = zi + RF_SLOT / 8;
+        f4 za[2][2], xb[4][2];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (kc + e < job.k) dst[e] = v[e];
+        for (int i = 0; i < 2; ++i) {
+            const float* p = zi + (g * H + (2 * wn + i) * 16 + c16) * 8;
+            za[i][0] = *reinterpret_cast<const f4*>(p);
+            za[i][1] = *reinterpret_cast<const f4*>(p + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = (4 * wk + j) * 16 + c16;
+            if (!staged) {
+                const float* p = xi + (g * H + c) * 8;
+                xb[j][0] = *reinterpret_cast<const f4*>(p);
+                xb[j][1] = *reinterpret_cast<const f4*>(p + 4);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xb[j][e >> 2][e & 3] = xi[(8 * g + e) * H + c];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(za[i][e >> 2][e & 3], xb[j][e >> 2][e & 3], acc[i][j],
+                                                                     0, 0, 0);
+        if (do_bias) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bsum[i] += za[i][e >> 2][e & 3];
         }
     }
-    if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (unconsumed) ring loads
+    __syncthreads();
+    ring_epilogue(job, chunk, acc, bsum, do_bias, wn, wk, lane, smem);
 }
 
 // grads[g] = Σ_c part[c][g] for g < G (blocks [0, ceil(G/64)): 64 outputs x 4 chunk groups each);
@@ -1698,8 +1815,9 @@ int launch_reduce(const mgn_mlp* m, const float* part, int nchunks, const float*
     return launch_reduce2(&d, 1, st);
 }
 
-// ring-kernel form of a single-MLP job list (bf16, h=128): every R8 job spans a full 128-column
-// block, re-gathered inputs are plain rows (no index). false: not eligible (generic kernel).
+// ring-kernel form of a single-MLP job list (h=128, bf16 or fp32): every R8 job spans a full
+// 128-column block, re-gathered inputs are plain rows (no index). false: not eligible (generic kernel).
+template <class T>
 bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
     constexpr int H = 128;
     if (a.H != H || a.M <= 0 || a.rows_per_chunk % RG_RS != 0 || nj > 12) return false;
@@ -1713,15 +1831,15 @@ bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
             int s = 0;
             while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
             const SrcSeg& g = a.seg[s];
-            if (g.idx != nullptr || g.ld % 8 != 0 || g.ld == 0) return false;
-            q.x = reinterpret_cast<const __bf16*>(g.p) + (col0 - g.coff);
+            if (g.idx != nullptr || g.ld % 8 != 0 || g.ld == 0 || g.dtype != dtype_id<T>()) return false;
+            q.x = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
             q.ld = g.ld;
         } else {
             if (col0 + H > jb.kp) return false;
-            q.x = reinterpret_cast<const __bf16*>(a.act8) + jb.act_off + (int64_t)col0 * 8;
+            q.x = reinterpret_cast<const T*>(a.act8) + jb.act_off + (int64_t)col0 * 8;
             q.ld = 0;
         }
-        q.z = reinterpret_cast<const __bf16*>(a.dz8) + (int64_t)jb.zl * a.RP * H;
+        q.z = reinterpret_cast<const T*>(a.dz8) + (int64_t)jb.zl * a.RP * H;
         q.RP = a.RP;
         q.M = a.M;
         q.part = a.part;
@@ -1739,14 +1857,20 @@ bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
     return true;
 }
 
-// prof_kind: PROF_WGRAD for the processor blocks' launch, PROF_WGRAD_DENSE for encoders / decoder
-int launch_ring(const RgArgs& r, hipStream_t st, int prof_kind = PROF_WGRAD_DENSE) {
-    if (int e = set_lds((const void*)wgrad_ring_kernel, RG_LDS)) return e;
+// prof_kind: PROF_WGRAD for the processor blocks' launch, PROF_WGRAD_DENSE for encoders / decoder;
+// f32: the fp32 ring (wgrad_ring_f32_kernel)
+int launch_ring(const RgArgs& r, hipStream_t st, int prof_kind = PROF_WGRAD_DENSE, bool f32 = false) {
+    const void* fn = f32 ? (const void*)wgrad_ring_f32_kernel : (const void*)wgrad_ring_kernel;
+    const size_t lds = f32 ? RF_LDS : RG_LDS;
+    if (int e = set_lds(fn, lds)) return e;
     int wgs = 0;
     for (int j = 0; j < r.njobs; ++j) wgs = r.job[j].wg0 + r.job[j].nchunks > wgs ? r.job[j].wg0 + r.job[j].nchunks : wgs;
     if (wgs == 0) return 0;
     ProfScope ps(prof_kind, st);
-    hipLaunchKernelGGL(wgrad_ring_kernel, dim3(wgs), dim3(512), RG_LDS, st, r);
+    if (f32)
+        hipLaunchKernelGGL(wgrad_ring_f32_kernel, dim3(wgs), dim3(512), lds, st, r);
+    else
+        hipLaunchKernelGGL(wgrad_ring_kernel, dim3(wgs), dim3(512), lds, st, r);
     MGN_LAUNCH_CHECK();
     return 0;
 }
@@ -1754,10 +1878,10 @@ int launch_ring(const RgArgs& r, hipStream_t st, int prof_kind = PROF_WGRAD_DENS
 template <class T, int H>
 int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
     a.njobs = nj;
-    if constexpr (sizeof(T) == 2 && H == 128) {
+    if constexpr (H == 128) {
         RgArgs r;
-        if (ring_jobs_from(a, nj, nchunks, r)) {
-            if (nchunks > 0 && nj > 0) return launch_ring(r, st);
+        if ((sizeof(T) == 2 || MGN_RING_F32) && ring_jobs_from<T>(a, nj, nchunks, r)) {
+            if (nchunks > 0 && nj > 0) return launch_ring(r, st, PROF_WGRAD_DENSE, sizeof(T) == 4);
             return 0;
         }
     }
@@ -1878,9 +2002,13 @@ struct BlockWgradIn {
     float *npart, *ngrads;
 };
 
+// T = __bf16: the chained bf16 blocks (dZ0 row-major, the bf16 ring); T = float: fp32 h=128 blocks on
+// the generic MLP kernels (every dZ in R8, incl. layer 0; the fp32 ring)
+template <class T>
 int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradIn& in, hipStream_t st,
                      RedDesc* defer = nullptr) {
     constexpr int H = 128;
+    constexpr bool F32 = sizeof(T) == 4;
     const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
     auto rows_for = [](int64_t RP, int64_t target, int* nch) {
         int64_t c = cdiv64(RP, target);
@@ -1936,21 +2064,22 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
         q.wg0 = wg;
         wg += nch;
     };
-    const __bf16* edz = reinterpret_cast<const __bf16*>(in.edz8);
-    const __bf16* ndz = reinterpret_cast<const __bf16*>(in.ndz8);
-    const __bf16* dP = reinterpret_cast<const __bf16*>(in.dP8);
+    const T* edz = reinterpret_cast<const T*>(in.edz8);
+    const T* ndz = reinterpret_cast<const T*>(in.ndz8);
+    const T* dP = reinterpret_cast<const T*>(in.dP8);
     const int64_t Ge = grad_G(edge), Gn = grad_G(node);
     // edge MLP over edge rows (heaviest first: dispatch order)
     int64_t off = 0;
     for (int l = 0; l < edge->n_layers; ++l) {
         int n, k;
         mlp_layer_shape(*edge, l, &n, &k);
-        const __bf16* z = edz + (int64_t)l * RPE * H;
+        const T* z = edz + (int64_t)l * RPE * H;
         if (l == 0) {
-            add(in.dz0, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0, re, ce);
-            r.job[nj - 1].zrm = 1;
+            add(F32 ? (const void*)z : in.dz0, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0,
+                re, ce);
+            r.job[nj - 1].zrm = F32 ? 0 : 1;
         } else
-            add(z, reinterpret_cast<const __bf16*>(in.eact) + act_off(*edge, in.E, l, 1), 0, RPE, in.E, in.epart, Ge,
+            add(z, reinterpret_cast<const T*>(in.eact) + act_off(*edge, in.E, l, 1), 0, RPE, in.E, in.epart, Ge,
                 off, off + (int64_t)n * k, n, k, act_cols(*edge, l), 0, re, ce);
         off += (int64_t)n * k + n;
     }
@@ -1959,12 +2088,12 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     for (int l = 0; l < node->n_layers; ++l) {
         int n, k;
         mlp_layer_shape(*node, l, &n, &k);
-        const __bf16* z = ndz + (int64_t)l * RPN * H;
+        const T* z = ndz + (int64_t)l * RPN * H;
         if (l == 0) {
             add(z, in.x, H, RPN, in.N, in.npart, Gn, off, off + (int64_t)n * k, n, k, k, 0, rn, cn);
             add(z, in.aggr, H, RPN, in.N, in.npart, Gn, off, -1, n, k, k, H, rn, cn);
         } else {
-            add(z, reinterpret_cast<const __bf16*>(in.nact) + act_off(*node, in.N, l, 1), 0, RPN, in.N, in.npart, Gn,
+            add(z, reinterpret_cast<const T*>(in.nact) + act_off(*node, in.N, l, 1), 0, RPN, in.N, in.npart, Gn,
                 off, off + (int64_t)n * k, n, k, act_cols(*node, l), 0, rn, cn);
         }
         off += (int64_t)n * k + n;
@@ -1974,7 +2103,7 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
         add(dP + (int64_t)s2 * RPN * H, in.x, H, RPN, in.N, in.epart, Ge, 0, -1, H, edge->in_dim, edge->in_dim,
             (1 + s2) * H, rp, cp);
     r.njobs = nj;
-    if (int e2 = launch_ring(r, st, PROF_WGRAD)) return e2;
+    if (int e2 = launch_ring(r, st, PROF_WGRAD, F32)) return e2;
     RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
                     red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
     // W0 [H][3H] of the edge MLP: its x-block columns [H, 3H) hold cp slabs (the projection jobs)
@@ -2555,14 +2684,24 @@ size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* 
 // the bandwidth-bound weight-gradient launch fills the CUs the latency-bound node kernels leave idle).
 struct BlockBwdCarve {
     void *mlp_ws, *dx_part, *d_aggr, *dz0, *dP8;
-    void* ndz;       // chained: node dZ saves (R8)
-    float* ndsp;     // chained: node dscale partials
-    float* npart;    // chained: node slabs
+    void* ndz;       // chained / ring32: node dZ saves (R8)
+    float* ndsp;     // chained / ring32: node dscale partials
+    float* npart;    // chained / ring32: node slabs
     void* dz8;       // edge dZ saves (R8)
     float* dsp;      // edge dscale partials
     float* part;     // edge slabs
-    bool chained;
+    bool chained;    // bf16 h=128 register-chained MLPs (+ the bf16 ring)
+    bool ring32;     // fp32 h=128 generic MLPs + the fp32 ring
 };
+
+// fp32 h=128 processor blocks (the reference's dtype): the node MLP's weight gradients join ONE fp32
+// ring launch per block with the edge MLP's and the W0 projections', as in the chained bf16 blocks
+static bool ring_f32_eligible(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    return MGN_RING_F32 && edge->dtype == MGN_F32 && node->dtype == MGN_F32 && edge->hidden == 128 &&
+           node->hidden == 128 && edge->n_layers == 4 && node->n_layers == 4 && edge->in_dim == 3 * 128 &&
+           node->in_dim == 2 * 128 && edge->out_dim == 128 && node->out_dim == 128 && t->num_nodes > 0 &&
+           t->num_edges > 0;
+}
 
 // Deferred-reduction "keep" buffer of one block: the RMSNorm-scale partial rows and the weight-
 // gradient slabs of both MLPs, which then outlive the block's call (the caller reduces every block's
@@ -2598,11 +2737,12 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dz0 = w + wl.dz0;
     c.dP8 = w + wl.dP8;
     c.chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
-    if (c.chained) {
+    c.ring32 = !c.chained && ring_f32_eligible(t, edge, node);
+    if (c.chained || c.ring32) {
         const int64_t Nn = t->num_nodes;
         char* q = w + wl.nmlp;
         c.ndz = q;
-        q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * 2);
+        q += align_up((size_t)node->n_layers * rows_pad(Nn) * H * (node->dtype == MGN_F32 ? 4 : 2));
         c.ndsp = reinterpret_cast<float*>(q);
         q += align_up((size_t)(rows_pad(Nn) / 16) * node->out_dim * sizeof(float));  // = mlp_bwd_ws carve
         c.npart = reinterpret_cast<float*>(q);
@@ -2616,7 +2756,7 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dsp = reinterpret_cast<float*>(p);
     p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
     c.part = reinterpret_cast<float*>(p);
-    if (keep && c.chained) {
+    if (keep && (c.chained || c.ring32)) {
         const KeepLayout k = keep_layout(t, edge, node);
         char* q = reinterpret_cast<char*>(keep);
         c.dsp = reinterpret_cast<float*>(q + k.edsp);
@@ -2660,6 +2800,16 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         int nparts = 0;
         if (int r = chain16_node_backward(node, t->num_nodes, &saved->node, dx_out, c.ndz, c.ndsp, &nparts, c.dx_part,
                                           c.d_aggr, st, flags & MGN_BWD_DX_OUT_PAIR))
+            return r;
+    } else if (c.ring32) {
+        // generic fp32 data gradients, dZ saves and dscale partials kept for the block's fp32 ring
+        MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, t->num_nodes), "backward workspace too small");
+        BwdOut on;
+        memset(&on, 0, sizeof(on));
+        on.mode = MODE_NODE;
+        on.o1 = c.dx_part;
+        on.o2 = c.d_aggr;
+        if (int r = mlp_bwd_any(node, MODE_NODE, t->num_nodes, &saved->node, dx_out, dt, H, on, c.ndz, c.ndsp, st))
             return r;
     } else {
         MlpIn nin;
@@ -2747,7 +2897,30 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         in.nntiles = chain16_node_backward_parts(N);
         in.npart = c.npart;
         in.ngrads = node_grads;
-        return block_wgrad_ring(edge, node, in, st, keep ? defer : nullptr);
+        return block_wgrad_ring<__bf16>(edge, node, in, st, keep ? defer : nullptr);
+    }
+    if (c.ring32) {
+        BlockWgradIn in;
+        in.E = E;
+        in.N = N;
+        in.e = e;
+        in.x = x;
+        in.aggr = saved->aggr;
+        in.eact = saved->edge.act;
+        in.edz8 = c.dz8;
+        in.dz0 = c.dz0;
+        in.dP8 = c.dP8;
+        in.edsp = c.dsp;
+        in.entiles = (int)(rows_pad(E) / bm_host(MGN_F32, MODE_EDGE));
+        in.epart = c.part;
+        in.egrads = edge_grads;
+        in.nact = saved->node.act;
+        in.ndz8 = c.ndz;
+        in.ndsp = c.ndsp;
+        in.nntiles = (int)(rows_pad(N) / bm_host(MGN_F32, MODE_NODE));
+        in.npart = c.npart;
+        in.ngrads = node_grads;
+        return block_wgrad_ring<float>(edge, node, in, st, keep ? defer : nullptr);
     }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
     const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
@@ -2805,7 +2978,8 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
     memset(reduce2, 0, 2 * sizeof(mgn_wgrad_reduce));
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
-    const bool chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
+    const bool chained = (chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0) ||
+                         ring_f32_eligible(t, edge, node);
     if (!chained) {  // generic MLPs: reduced at once, nothing left for the caller
         MGN_REQUIRE(!flags, "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
         if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,
