@@ -1098,6 +1098,12 @@ struct RgArgs {
     RgJob job[12];
 };
 
+// fp32 single-MLP job lists that mix 128-column jobs with narrower ones (A/B builds: 0 = all on the
+// generic kernel)
+#ifndef MGN_RING_SPLIT
+#define MGN_RING_SPLIT 1
+#endif
+
 // fp32 ring (wgrad_ring_f32_kernel) for fp32 h=128 MLPs (A/B builds: 0 = the generic weight-gradient
 // kernel, 3 launches + 2 reductions per block)
 #ifndef MGN_RING_F32
@@ -1817,6 +1823,27 @@ int launch_reduce(const mgn_mlp* m, const float* part, int nchunks, const float*
 
 // ring-kernel form of a single-MLP job list (h=128, bf16 or fp32): every R8 job spans a full
 // 128-column block, re-gathered inputs are plain rows (no index). false: not eligible (generic kernel).
+// job j of a: its X operand as the ring reads it (a full 128-column block), or false
+template <class T>
+bool ring_job_x(const WgArgs& a, const WgJob& jb, const void** x, int64_t* ld) {
+    constexpr int H = 128;
+    const int col0 = jb.kb * H;
+    if (jb.staged) {
+        int s = 0;
+        while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
+        const SrcSeg& g = a.seg[s];
+        if (g.idx != nullptr || g.ld % 8 != 0 || g.ld == 0 || g.dtype != dtype_id<T>() || col0 - g.coff + H > g.ncols)
+            return false;
+        *x = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
+        *ld = g.ld;
+    } else {
+        if (col0 + H > jb.kp) return false;
+        *x = reinterpret_cast<const T*>(a.act8) + jb.act_off + (int64_t)col0 * 8;
+        *ld = 0;
+    }
+    return true;
+}
+
 template <class T>
 bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
     constexpr int H = 128;
@@ -1827,18 +1854,7 @@ bool ring_jobs_from(const WgArgs& a, int nj, int nchunks, RgArgs& r) {
         const WgJob& jb = a.job[j];
         RgJob& q = r.job[j];
         const int col0 = jb.kb * H;
-        if (jb.staged) {
-            int s = 0;
-            while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
-            const SrcSeg& g = a.seg[s];
-            if (g.idx != nullptr || g.ld % 8 != 0 || g.ld == 0 || g.dtype != dtype_id<T>()) return false;
-            q.x = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
-            q.ld = g.ld;
-        } else {
-            if (col0 + H > jb.kp) return false;
-            q.x = reinterpret_cast<const T*>(a.act8) + jb.act_off + (int64_t)col0 * 8;
-            q.ld = 0;
-        }
+        if (!ring_job_x<T>(a, jb, &q.x, &q.ld)) return false;
         q.z = reinterpret_cast<const T*>(a.dz8) + (int64_t)jb.zl * a.RP * H;
         q.RP = a.RP;
         q.M = a.M;
@@ -1883,6 +1899,28 @@ int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
         if ((sizeof(T) == 2 || MGN_RING_F32) && ring_jobs_from<T>(a, nj, nchunks, r)) {
             if (nchunks > 0 && nj > 0) return launch_ring(r, st, PROF_WGRAD_DENSE, sizeof(T) == 4);
             return 0;
+        }
+        // mixed fp32 job lists (the encoders: a layer-0 input narrower than 128 columns): the
+        // 128-column jobs on the fp32 ring, the rest on the generic kernel, into the same slabs
+        // (disjoint columns): fp32 encoders 163 -> 74 us per launch. bf16: no faster (the generic
+        // bf16 kernel is 22 us), so the bf16 encoders keep one launch.
+        if (MGN_RING_SPLIT && sizeof(T) == 4 && MGN_RING_F32 && nchunks > 0 && nj > 1) {
+            WgArgs ra = a, ga = a;
+            int nr = 0, ng = 0;
+            for (int j = 0; j < nj; ++j) {
+                const void* x;
+                int64_t ld;
+                if (ring_job_x<T>(a, a.job[j], &x, &ld))
+                    ra.job[nr++] = a.job[j];
+                else
+                    ga.job[ng++] = a.job[j];
+            }
+            if (nr > 0 && ng > 0 && ring_jobs_from<T>(ra, nr, nchunks, r)) {
+                if (int e = launch_ring(r, st, PROF_WGRAD_DENSE, sizeof(T) == 4)) return e;
+                a = ga;
+                nj = ng;
+                a.njobs = nj;
+            }
         }
     }
     auto fn = mlp_wgrad_kernel<T, H>;
