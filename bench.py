@@ -338,11 +338,18 @@ def main():
     from graphphysics import _native as nat
     from graphphysics.utils import meshes
 
+    t_start = time.perf_counter()
+
+    def log(msg):  # progress on stderr (the JSON line stays the only stdout line)
+        print("[bench rank %d %.1fs] %s" % (rank, time.perf_counter() - t_start, msg), file=sys.stderr, flush=True)
+
     nat.load()
     mesh = meshes.load_cylinder_mesh()
     step, sim, b, data, lay, workload, datadesc = build_step(a, dev, rank, mesh, world)
     N, E = data.x.shape[0], data.edge_index.shape[1]
+    log("step built (N=%d, E=%d, world=%d)" % (N, E, world))
     warm(a, step)
+    log("warm-up done (%s)" % ("graph captured" if step.use_graph else "eager"))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -362,6 +369,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    log("timed steps done: %.3f ms/step" % (1000 * dt / a.steps))
     # sustained rate: the same step replayed for about `sustain` more seconds (reported beside the
     # headline, never as `value`; it also keeps the GPU visibly busy for the driver's sampler)
     sus = None
@@ -379,6 +387,7 @@ def main():
             dist.barrier()
         ds = time.perf_counter() - t1
         sus = {"steps": n_s, "seconds": round(ds, 3), "value": round(world * n_s / ds, 3), "unit": "steps/s"}
+        log("sustained: %d steps in %.2f s" % (n_s, ds))
     prof = profile_classes(a, step) if not a.no_profile else {}
     if world > 1:
         t = torch.tensor([dt], device=dev)
