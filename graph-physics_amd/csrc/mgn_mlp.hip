@@ -1580,12 +1580,15 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 #ifndef MGN_BF16_BM
 #define MGN_BF16_BM 64  // rows per workgroup of the generic bf16 dense / edge kernels (A/B builds: 32)
 #endif
+#ifndef MGN_F32_BM
+#define MGN_F32_BM 32  // rows per workgroup of the generic fp32 dense / edge kernels (A/B builds: 64)
+#endif
 template <class T>
-constexpr int bm_of() { return sizeof(T) == 4 ? 32 : MGN_BF16_BM; }
-// rows per workgroup tile: bf16 node MLPs use 32 (N is ~6x smaller than E: twice the workgroups)
+constexpr int bm_of() { return sizeof(T) == 4 ? MGN_F32_BM : MGN_BF16_BM; }
+// rows per workgroup tile: node MLPs use 32 (N is ~6x smaller than E: twice the workgroups)
 template <class T, int MODE>
 constexpr int bm_for() { return MODE == MODE_NODE ? 32 : bm_of<T>(); }
-int bm_host(int dtype, int mode) { return dtype == MGN_F32 || mode == MODE_NODE ? 32 : MGN_BF16_BM; }
+int bm_host(int dtype, int mode) { return mode == MODE_NODE ? 32 : dtype == MGN_F32 ? MGN_F32_BM : MGN_BF16_BM; }
 
 // Raise a kernel's dynamic-LDS limit once (not per launch: launches may be inside a graph capture).
 int set_lds(const void* fn, size_t bytes) {
@@ -2787,7 +2790,7 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     }
     const int64_t E = t->num_edges;
     const size_t es = dt == MGN_F32 ? 4 : 2;
-    const int ntiles = (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
+    const int ntiles = (int)(rows_pad(E) / bm_host(dt, MODE_EDGE));
     char* p = reinterpret_cast<char*>(c.mlp_ws);
     c.dz8 = p;
     p += align_up((size_t)edge->n_layers * rows_pad(E) * H * es);
@@ -2961,7 +2964,7 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         return block_wgrad_ring<float>(edge, node, in, st, keep ? defer : nullptr);
     }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
-    const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / (dt == MGN_F32 ? 32 : 64));
+    const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / bm_host(dt, MODE_EDGE));
     MlpIn ein;
     memset(&ein, 0, sizeof(ein));
     ein.seg[0] = SrcSeg{e, nullptr, H, H, dt, 0, 0};
