@@ -28,6 +28,10 @@ namespace {
 enum { MODE_DENSE = 0, MODE_EDGE = 1, MODE_NODE = 2 };
 
 template <int NT, int MT>
+#ifndef MGN_F32_PD
+#define MGN_F32_PD 8  // weight k-steps in flight in the generic fp32 GEMMs (A/B: 4 -> 86.8, 8 -> 90.0, 16 -> 88.5 steps/s)
+#endif
+
 struct TileCfg {
     static constexpr int WN = NT < 4 ? NT : 4;
     static constexpr int NTW = NT / WN;
@@ -65,8 +69,9 @@ struct Gemm {
         const T* bp = lds + (size_t)(mt0 * 16 + (lane & 15)) * ldl + VEC * (lane >> 4);
         const T* ap = wp + ((size_t)nt0 * kstride * 64 + lane) * VEC;
         // weight fragments come from L2: keep PD k-steps of them in flight (register ring with
-        // compile-time slots; the k loop is unrolled by PD so every ring index is static)
-        constexpr int PD = 4;
+        // compile-time slots; the k loop is unrolled by PD so every ring index is static). An fp32
+        // fragment is one VGPR (K = 4 per k-step), so fp32 keeps MGN_F32_PD k-steps in flight.
+        constexpr int PD = sizeof(T) == 4 ? MGN_F32_PD : 4;
         typename Mf<T>::frag ring[PD][C::NTW];
 #pragma unroll
         for (int u = 0; u < PD; ++u)
