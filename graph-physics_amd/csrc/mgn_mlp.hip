@@ -31,6 +31,9 @@ template <int NT, int MT>
 #ifndef MGN_F32_PD
 #define MGN_F32_PD 8  // weight k-steps in flight in the generic fp32 GEMMs (A/B: 4 -> 86.8, 8 -> 90.0, 16 -> 88.5 steps/s)
 #endif
+#ifndef MGN_BF16_PD
+#define MGN_BF16_PD 4  // the same for bf16 (one fragment = 4 VGPRs)
+#endif
 
 struct TileCfg {
     static constexpr int WN = NT < 4 ? NT : 4;
@@ -71,7 +74,7 @@ struct Gemm {
         // weight fragments come from L2: keep PD k-steps of them in flight (register ring with
         // compile-time slots; the k loop is unrolled by PD so every ring index is static). An fp32
         // fragment is one VGPR (K = 4 per k-step), so fp32 keeps MGN_F32_PD k-steps in flight.
-        constexpr int PD = sizeof(T) == 4 ? MGN_F32_PD : 4;
+        constexpr int PD = sizeof(T) == 4 ? MGN_F32_PD : MGN_BF16_PD;
         typename Mf<T>::frag ring[PD][C::NTW];
 #pragma unroll
         for (int u = 0; u < PD; ++u)
