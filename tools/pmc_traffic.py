@@ -33,13 +33,16 @@ def sources_sha():
 
 def kernel_class(name):
     """bench.py / libmgn profiler class of a kernel instance (None: not a training-step class)."""
-    m = re.search(r"mlp_(fwd|bwd)_kernel.*?Li(\d+)ELi(\d+)ELi(\d)E", name)
+    # generic MLP kernels, mangled (..._kernelIfLi128ELi32ELi1E...) or demangled (<float, 128, 32, 1>)
+    m = re.search(r"mlp_(fwd|bwd)_kernel(?:.*?Li(\d+)ELi(\d+)ELi(\d)E|<[^,<>]+, (\d+), (\d+), (\d)>)", name)
     if m:
-        return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[m.group(4)]
+        mode = m.group(4) or m.group(7)
+        return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[mode]
     for key, cls in (("chain16_node_fwd_kernel", "fwd_node"), ("chain16_node_bwd_kernel", "bwd_node"),
                      ("chain16_dense_fwd_kernel", "fwd_dense"), ("chain16_dense_bwd_kernel", "bwd_dense"),
                      ("chain16_fwd_kernel", "fwd_edge"), ("chain16_bwd_kernel", "bwd_edge"),
                      ("mlp_wgrad_kernel", "wgrad_dense"), ("wgrad_ring_kernel", "wgrad"),
+                     ("wgrad_ring_f32_kernel", "wgrad"),
                      ("wgrad_reduce_kernel", "wgrad_reduce"), ("node_grad_kernel", "combine"),
                      ("node_proj_kernel", "proj"), ("adamw", "adamw"), ("pack_kernel", "pack")):
         if key in name:
