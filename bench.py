@@ -150,6 +150,39 @@ def scatter_bytes(n, e, h, es):
     return e * h * es + n * h * es + 4 * e + 4 * (n + 1)
 
 
+def scatter_standalone(a, data, dev):
+    """The same segmented sum as a kernel of its own (`mgn_segment_sum`, the ABI's scatter_add
+    replacement: one thread per segment and 16-byte chunk, rows read in CSC order) over the step's
+    topology and an [E, h] message tensor of the compute dtype: HIP-event time of 50 launches."""
+    from graphphysics import _native as nat
+    from graphphysics.models import _engine
+
+    N, E, h = data.x.shape[0], data.edge_index.shape[1], a.hidden
+    tdt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    topo = _engine.get_topology(data.edge_index, N)
+    z = torch.randn(E, h, device=dev).to(tdt)
+    out = torch.empty(N, h, device=dev, dtype=tdt)
+    mdt = nat.MGN_BF16 if a.dtype == "bf16" else nat.MGN_F32
+    st = nat.stream_ptr(dev)
+
+    def run():
+        nat.check(nat.lib().mgn_segment_sum(nat.ptr(z), nat.ptr(topo.col_ptr), N, h, mdt, nat.ptr(out), st))
+
+    for _ in range(5):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1000 / 50
+    sb = scatter_bytes(N, E, h, 2 if a.dtype == "bf16" else 4)
+    return {"kernel": "mgn_segment_sum (standalone, same topology and sizes)", "bytes_per_launch": sb,
+            "avg_launch_us": round(t * 1e6, 2), "achieved": round(sb / t / 1e9, 1), "peak": HBM_PEAK, "unit": "GB/s",
+            "frac": round(sb / t / 1e9 / HBM_PEAK, 4)}
+
+
 def build_step(a, dev, rank, mesh, world):
     """Workload + Simulator + FusedAdamW + schedule + TrainStep of configuration `a`."""
     from graphphysics.models.processors import EncodeProcessDecode
@@ -424,6 +457,8 @@ def main():
     if sus is not None:
         out["sustained"] = sus
 
+    if world == 1 and roof is not None:
+        roof["scatter_standalone"] = scatter_standalone(a, data, dev)
     if not a.no_mse and a.workload == "cylinder":
         out["one_step_mse"] = one_step_mse(sim, mesh, dev, a)
     if world == 1 and a.cpu_steps > 0:

@@ -86,7 +86,8 @@ class FusedAdamW(torch.optim.Optimizer):
             else:
                 for p in ps:
                     s = self.state[p]
-                    nat.check(L.mgn_adamw_dev(nat.ptr(p), nat.ptr(p.grad.contiguous()), nat.ptr(s["exp_avg"]),
+                    g = p.grad.contiguous()  # held until the launch is enqueued
+                    nat.check(L.mgn_adamw_dev(nat.ptr(p), nat.ptr(g), nat.ptr(s["exp_avg"]),
                                               nat.ptr(s["exp_avg_sq"]), p.numel(), nat.ptr(hyper), b1, b2,
                                               group["eps"], group["weight_decay"], err, st))
 

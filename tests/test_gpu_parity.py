@@ -453,16 +453,43 @@ def test_segment_sum_and_permute():
     cuts = torch.sort(torch.randint(0, rows + 1, (segs - 1,), generator=g)).values
     ptr = torch.cat([torch.tensor([0]), cuts, torch.tensor([rows])]).int()
     out = torch.empty(segs, cols, device=DEV)
-    nat.check(L.mgn_segment_sum(nat.ptr(src.to(DEV)), nat.ptr(ptr.to(DEV)), segs, cols, nat.MGN_F32,
-                                nat.ptr(out), nat.stream_ptr()))
+    srcd, ptrd = src.to(DEV), ptr.to(DEV)  # held: a temporary's memory may be reused before the launch
+    nat.check(L.mgn_segment_sum(nat.ptr(srcd), nat.ptr(ptrd), segs, cols, nat.MGN_F32, nat.ptr(out),
+                                nat.stream_ptr()))
     ref = torch.stack([src[ptr[i]:ptr[i + 1]].sum(0) for i in range(segs)])
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-5)
     idx = torch.randperm(rows, generator=g).int()
     srcd = src.to(DEV)
     gath = torch.empty(rows, cols, device=DEV)
-    nat.check(L.mgn_permute_rows(nat.ptr(srcd), nat.ptr(gath), nat.ptr(idx.to(DEV)), rows, cols, nat.MGN_F32,
+    idxd = idx.to(DEV)
+    nat.check(L.mgn_permute_rows(nat.ptr(srcd), nat.ptr(gath), nat.ptr(idxd), rows, cols, nat.MGN_F32,
                                  nat.MGN_F32, 0, nat.stream_ptr()))
     assert torch.equal(gath.cpu(), src[idx.long()])
+
+
+@pytest.mark.parametrize("cols,dtype", [(128, torch.float32), (128, torch.bfloat16), (24, torch.bfloat16),
+                                        (3, torch.float32), (3, torch.bfloat16)])
+def test_segment_sum_bitexact_vs_scatter_add(cols, dtype):
+    """mgn_segment_sum (16-byte-chunk kernel when cols fill whole chunks, else the scalar one) equals
+    ATen's scatter_add_ in fp32 over the same rows in increasing order, bit for bit, then rounded to the
+    output dtype once: empty segments, degree-1 segments and long ones (up to 37 rows)."""
+    from graphphysics import _native as nat
+
+    g = torch.Generator().manual_seed(11)
+    segs = 700
+    deg = torch.randint(0, 8, (segs,), generator=g)
+    deg[::50] = 37
+    deg[1::97] = 0
+    ptr = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(deg, 0)]).int()
+    rows = int(ptr[-1])
+    src = torch.randn(rows, cols, generator=g).to(dtype)
+    seg_of_row = torch.repeat_interleave(torch.arange(segs), deg)
+    ref = torch.zeros(segs, cols).scatter_add_(0, seg_of_row[:, None].expand(-1, cols), src.float()).to(dtype)
+    out = torch.empty(segs, cols, device=DEV, dtype=dtype)
+    srcd, ptrd = src.to(DEV), ptr.to(DEV)  # held: a temporary's memory may be reused before the launch
+    nat.check(nat.lib().mgn_segment_sum(nat.ptr(srcd), nat.ptr(ptrd), segs, cols, nat.mgn_dtype(dtype), nat.ptr(out),
+                                        nat.stream_ptr()))
+    assert torch.equal(out.cpu(), ref)
 
 
 def test_empty_edge_set():
