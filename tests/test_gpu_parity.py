@@ -424,6 +424,41 @@ def test_epd_bf16_h128_more_nodes_than_edges(n, e):
         assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
 
 
+@pytest.mark.parametrize("n,e", [(1100, 1000), (3000, 700)])
+def test_epd_fp32_h128_more_nodes_than_edges(n, e):
+    """The fp32 weight-gradient ring (fp32 h=128 blocks: one ring launch per block, projection jobs
+    over node rows into the edge slab buffer, chunk count capped at the edge slabs) on graphs with more
+    nodes than edges: output vs the fp32 oracle (1e-4) and every gradient no further from fp64 than
+    the reference's own fp32 path (assert_vs_truth)."""
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    g = torch.Generator().manual_seed(13)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(e, 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    mp, h = 2, 128
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    rp = dict(ref.named_parameters())
+    yr = O.encode_process_decode(x, ei, ea, rp, mp)
+    (yr * gy).sum().backward()
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(x.double(), ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=torch.float32).to(DEV)
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        y = m(Data(x=x.to(DEV), edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+        (y * gy.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert relerr(y, yr) < 1e-4
+    for k, p in m.named_parameters():
+        assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, tie_tol=2e-3)
+
+
 # ----------------------------------------------------------------------------- optimiser / primitives
 def test_adamw_matches_torch():
     from graphphysics.training.optim import FusedAdamW
