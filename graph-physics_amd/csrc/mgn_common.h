@@ -118,12 +118,19 @@ __host__ __device__ __forceinline__ int rup(int a, int b) { return cdiv(a, b) * 
 // Transposed fragments (A operand of dX = dY·W):
 //   packT[((kt*NS + ns)*64 + lane)*VEC + v] = W[ns*KSTEP + VEC*(lane>>4) + v][kt*16 + (lane&15)]
 // kt runs over round_up(ceil(K/16), 8) tiles so a backward chunk of hidden/16 tiles never reads
-// past the layer. Both use the same per-layer element count.
+// past the layer. Both use the same per-layer element count. An fp32 Linear with n == 128 and k a
+// multiple of 128 also carries a 128x128 "chain image" of its first 128 input columns after the
+// fragments of either region (the register-chained fp32 edge kernels' LDS-DMA source, mgn_mlp.hip):
+//   image[((nt*8 + t)*64 + lane)*4 + r]  = W[nt*16 + (lane&15)][t*16 + 4*(lane>>4) + r]   (forward)
+//   imageT[((kt*8 + t)*64 + lane)*4 + r] = W[t*16 + 4*(lane>>4) + r][kt*16 + (lane&15)]   (transposed)
+__host__ __device__ inline bool has_chain_image(int n, int k, int dtype) {
+    return dtype == MGN_F32 && n == 128 && k > 0 && k % 128 == 0;
+}
 __host__ __device__ inline int64_t linear_pack_elems(int n, int k, int dtype) {
     const int vec = dtype == MGN_BF16 ? 8 : 1, kstep = 4 * vec;
     int64_t fwd = (int64_t)cdiv(n, 16) * cdiv(k, kstep);
     int64_t bwd = (int64_t)rup(cdiv(k, 16), 8) * cdiv(n, kstep);
-    return (fwd > bwd ? fwd : bwd) * 64 * vec;
+    return (fwd > bwd ? fwd : bwd) * 64 * vec + (has_chain_image(n, k, dtype) ? 128 * 128 : 0);
 }
 
 // Layer shapes of build_mlp(in, hidden, out, L)

@@ -1547,9 +1547,17 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
     // one Linear's pack is far below 2^31 elements: 32-bit index math (64-bit divisions by the
     // runtime KS / NS cost tens of instructions each)
     const int tot = (int)linear_pack_elems(n, k, dtype_id<T>());
+    const int img0 = has_chain_image(n, k, dtype_id<T>()) ? tot - 128 * 128 : tot;  // chain image start
     T* dst = reinterpret_cast<T*>(j.dst);
     T* dstT = reinterpret_cast<T*>(j.dstT);
     for (int e = blockIdx.x * MGN_THREADS + threadIdx.x; e < tot; e += gridDim.x * MGN_THREADS) {
+        if (e >= img0) {  // chain images (mgn_common.h): first 128 input columns, permuted k-steps
+            const int i = e - img0, r = i & 3, lane = (i >> 2) & 63, t = (i >> 8) & 7, b = i >> 11;
+            const int a16 = b * 16 + (lane & 15), c = t * 16 + 4 * (lane >> 4) + r;
+            dst[e] = from_f<T>(pack_src(j, a16, c));   // W[a16][c]
+            dstT[e] = from_f<T>(pack_src(j, c, a16));  // W[c][a16]
+            continue;
+        }
         const int v = e % VEC;
         const int fl = e / VEC;
         const int lane = fl % 64;
@@ -1582,6 +1590,363 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
         pack_job<float>(j);
     else
         pack_job<__bf16>(j);
+}
+
+// --------------------------------------------------------------------------- fp32 edge MLP, register-chained
+// The fp32 GraphNetBlock edge MLP at h = 128 (4 Linears + RMSNorm, reference layers.py:652-658,
+// 703-719): each wave owns 16 edge rows through all four layers; activations never leave registers.
+// Layer l computes D^T[n][row] = Σ_k W[n][k]·X[row][k] with v_mfma_f32_16x16x4_f32; its C layout
+// (lane l, reg r: feature 16nt + 4(l>>4) + r of row l&15) is, unchanged, the B operand of layer l+1
+// when that layer's k-step (t, r) covers k = 16t + 4(l>>4) + r: a GEMM's k axis may be summed in any
+// order, so only the A operand (the weights) follows the permutation. The pack kernel writes each
+// 128-wide fp32 Linear's first 128 input columns once more in that order (the "chain image", after the
+// fragments: lane l's four k-steps (t, r = 0..3) of n-tile nt as one 16-byte word, forward
+// W[16nt + (l&15)][16t + 4(l>>4) + r], transposed W[16t + 4(l>>4) + r][16nt + (l&15)]); a 12-wave
+// workgroup streams layer l+1's 64 KiB image into LDS by LDS-DMA while layer l's MFMAs run (double
+// buffer, one barrier per layer). Measured on the way (Cfg B, fp32 step): weights streamed from L2 per
+// wave (four dword loads per 4 MFMAs) 227–238 µs per edge forward vs 173 µs for the generic kernel;
+// register-staged permutation through ds_write, 8 waves: 169.5 / 187 µs (forward / backward vs 173 /
+// 186); the same with 4-wave workgroups spilled 200+ bytes per lane.
+#ifndef MGN_F32_CHAIN
+#define MGN_F32_CHAIN 1  // 0: the fp32 edge MLP on the generic LDS-tiled kernels (A/B builds)
+#endif
+#ifdef MGN_STAMPS  // diagnostics builds: per-phase s_memtime deltas of wave 0 of workgroup 0 (as mgn_chain16.hip)
+#define F32C_STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define F32C_STAMP(i)                                                                     \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        unsigned long long st_t;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");     \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        st_ph[i] += st_t - st_prev;                                                       \
+        st_prev = st_t;                                                                   \
+    } while (0)
+#define F32C_STAMP_PRINT(name)                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                                                     \
+    printf("%s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", name, st_ph[0], st_ph[1], st_ph[2], \
+           st_ph[3], st_ph[4], st_ph[5], st_ph[6], st_ph[7], st_ph[8], st_ph[9], st_ph[10], st_ph[11])
+#else
+#define F32C_STAMP_DECL
+#define F32C_STAMP(i)
+#define F32C_STAMP_PRINT(name)
+#endif
+constexpr int F32C_WAVES = 12;         // three waves per SIMD (168 VGPRs), 192 rows per workgroup
+constexpr int F32C_LAYER = 128 * 128;  // floats per chain image (64 KiB)
+
+// The chain image of a pack region (fwd or transposed) of a fp32 [n][k] Linear, or NULL: it follows
+// the fragments (linear_pack_elems counts it: n == 128, k a multiple of 128).
+__host__ __device__ inline int64_t chain_image_off(int n, int k) {
+    return linear_pack_elems(n, k, MGN_F32) - F32C_LAYER;
+}
+
+// Issue this wave's share of one 64 KiB image copy global -> LDS (1 KiB per LDS-DMA instruction).
+__device__ __forceinline__ void f32c_stage(const float* __restrict__ src, float* img) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = wave; c < F32C_LAYER / 256; c += F32C_WAVES)
+        glds16(src + c * 256 + lane * 4, img + c * 256);
+}
+__device__ __forceinline__ void f32c_stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// acc[nt] += D^T tile nt of X·Wᵀ (16 rows) from the LDS image; x[t][r] = B operand of k-step (t, r).
+// save != NULL: also store the operand to its R8 save (save = the lane's R8 address of column 4(l>>4);
+// x[t][r] is column 16t + 4(l>>4) + r), four dwords per k-step group, spreading the saves over the
+// MFMAs (stored at once after each layer, every wave of the chip writes at the same time).
+__device__ __forceinline__ void f32c_gemm(f4 (&acc)[8], const f4 (&x)[8], const float* img, int lane,
+                                          float* save = nullptr) {
+    // LDS reads run one half k-step group ahead (n-tiles 0..3, then 4..7: 16 MFMAs per half)
+    f4 w[2][4];
+    const f4* ip = reinterpret_cast<const f4*>(img) + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[0][j] = ip[(j * 8 + 0) * 64];
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+        const int t = h >> 1, n0 = (h & 1) * 4;
+        if (h + 1 < 16) {
+            const int t1 = (h + 1) >> 1, n1 = ((h + 1) & 1) * 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[(h + 1) & 1][j] = ip[((n1 + j) * 8 + t1) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the next LDS reads stay ahead of these MFMAs
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[n0 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[h & 1][j][r], x[t][r], acc[n0 + j], 0, 0, 0);
+        if (save && (h & 1)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) save[128 * t + 8 * r] = x[t][r];
+        }
+    }
+}
+
+__global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(FwdArgs a) {
+    constexpr int H = 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* const img0 = reinterpret_cast<float*>(smem);
+    float* const img1 = img0 + F32C_LAYER;
+    float* const vec = img1 + F32C_LAYER;  // [5][H]: biases b0..b3, RMSNorm scale (LDS: no VMEM loads
+                                           // behind the saves' stores, which would wait for them)
+    const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15;
+    const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + (threadIdx.x >> 6);
+    const int64_t row0 = tile * 16, row = row0 + ri;
+    const bool live = row0 < rows_pad(a.M);  // tiles past the padded rows only join the barriers
+    const bool valid = row < a.M;
+    F32C_STAMP_DECL;
+    const float* pk = reinterpret_cast<const float*>(a.wpack);
+    f32c_stage(pk + chain_image_off(H, a.Kpack0), img0);  // layer 0: W0's e-column block
+    pk += linear_pack_elems(H, a.Kpack0, MGN_F32);
+    int32_t pi = 0, pj = 0;
+    if (valid) {
+        pi = a.proj_i[row];
+        pj = a.proj_j[row];
+    }
+    const float* e = reinterpret_cast<const float*>(a.seg[0].p);
+    f4 x[8], acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        x[t] = valid ? *reinterpret_cast<const f4*>(e + row * a.seg[0].ld + 16 * t + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
+    // layer 0's accumulator starts at P_i + P_j + b0: [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]
+    {
+        const f4* ppi = reinterpret_cast<const f4*>(a.proj + (int64_t)pi * (2 * H)) + g;
+        const f4* ppj = reinterpret_cast<const f4*>(a.proj + (int64_t)pj * (2 * H) + H) + g;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = valid ? ppi[4 * nt] : f4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_sched_barrier(0);  // two passes: 32 registers of gathers in flight, not 64
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt)
+            if (valid) acc[nt] += ppj[4 * nt];
+    }
+    for (int i = threadIdx.x; i < 5 * H; i += F32C_WAVES * 64) {
+        const int vl = i >> 7;
+        const float* vp = vl == 0 ? a.bias[0] : vl == 1 ? a.bias[1] : vl == 2 ? a.bias[2] : vl == 3 ? a.bias[3] : a.scale;
+        vec[i] = vp[i & (H - 1)];
+    }
+    f32c_stage_wait();
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) acc[nt] += *reinterpret_cast<const f4*>(vec + 16 * nt + 4 * g);
+    F32C_STAMP(0);
+    float* act = reinterpret_cast<float*>(a.act8);
+    const int64_t r8 = ((row >> 3) * H + 4 * g) * 8 + (row & 7);  // R8 index of (row, 4g)
+    const float* res = reinterpret_cast<const float*>(a.resid);
+    f4 rv[8];
+#pragma unroll 1
+    for (int l = 0; l < 4; ++l) {
+        if (l < 3) {
+            // layer l+1's image streams into the other buffer during this layer's MFMAs (its readers,
+            // layer l-1, passed the last barrier)
+            f32c_stage(pk + chain_image_off(H, H), (l & 1) ? img0 : img1);
+            pk += linear_pack_elems(H, H, MGN_F32);
+        } else {
+            // the residual lands during the last GEMM
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt)
+                rv[nt] = (res && valid) ? *reinterpret_cast<const f4*>(res + row * H + 16 * nt + 4 * g)
+                                        : f4{0.f, 0.f, 0.f, 0.f};
+        }
+        // layer l's input (the ReLU output of layer l-1) is saved while it feeds the MFMAs
+        // (save pointers by selection: a kernel-argument array indexed at run time is copied to scratch)
+        float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
+        f32c_gemm(acc, x, (l & 1) ? img1 : img0, lane, (l > 0 && live) ? sv + r8 : nullptr);
+        F32C_STAMP(1);
+        if (l < 3) {
+            unsigned long long word = 0;
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float v = fmaxf(acc[nt][r], 0.f);
+                    x[nt][r] = v;
+                    const unsigned long long bits = __ballot(v > 0.f);
+                    if (lane == nt * 4 + r) word = bits;
+                }
+                acc[nt] = *reinterpret_cast<const f4*>(vec + (l + 1) * H + 16 * nt + 4 * g);
+            }
+            // the tile's 32 ballot words of layer l: word nt*4 + r from lane nt*4 + r
+            if (live && lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
+            F32C_STAMP(2);
+            f32c_stage_wait();
+            __syncthreads();
+            F32C_STAMP(3);
+        }
+    }
+    // last Linear (bias in the accumulator): RMSNorm over the row's 128 features (4 lanes of 32), residual
+    float ss = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss += acc[nt][r] * acc[nt][r];
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    if (valid) {
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        if (g == 0) a.rden_save[row] = q;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + n);
+            f4 y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = s[r] * (acc[nt][r] / q);
+            y = rv[nt] + y;
+            st4(reinterpret_cast<float*>(a.z_save) + row * H + n, acc[nt]);
+            if (a.out_dtype == MGN_BF16)
+                st4(reinterpret_cast<__bf16*>(a.out) + row * a.out_ld + n, y);
+            else
+                st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
+        }
+    }
+    F32C_STAMP(4);
+    F32C_STAMP_PRINT("f32f");
+}
+
+// Backward of the same MLP (data gradients; the weight gradients run on the fp32 ring from the dZ
+// saves): the RMSNorm backward gives dZ3 in the C layout, and dH_l^T[k][row] = Σ_n W_l[n][k]·dZ_l[row][n]
+// chains exactly like the forward with the transposed chain images. Outputs match mlp_bwd_kernel: dZ_l
+// R8 saves, dZ_0 row-major, de_in = dout + dZ_0·W0a, and RMSNorm-scale partials per 32 rows (the
+// generic kernel's partial count: two waves combine in LDS).
+__global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(BwdArgs a) {
+    constexpr int H = 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* const img0 = reinterpret_cast<float*>(smem);
+    float* const img1 = img0 + F32C_LAYER;
+    float* const red = img1 + F32C_LAYER;  // [F32C_WAVES][H] per-wave RMSNorm-scale partials
+    const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15, wave = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + wave;
+    const int64_t row0 = tile * 16, row = row0 + ri;
+    const bool live = row0 < a.RP;
+    const bool valid = row < a.M;
+    F32C_STAMP_DECL;
+    const float* wt = reinterpret_cast<const float*>(a.wtpack);
+    int64_t off[4];
+    {
+        int64_t o = 0;
+        for (int l = 0; l < 4; ++l) {
+            off[l] = o;
+            o += linear_pack_elems(H, l == 0 ? a.Kpack0 : H, MGN_F32);
+        }
+    }
+    f32c_stage(wt + off[3] + chain_image_off(H, H), img0);
+    // the tile's ReLU mask words of hidden layers 0..2 (word nt*4 + r in lane nt*4 + r), loaded before
+    // any store: a VMEM load issued behind stores waits for them
+    unsigned long long mw[3] = {0ull, 0ull, 0ull};
+    if (live && lane < 32) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mw[l] = a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane];
+    }
+    // ---- dY = dout + d_aggr[dst] -> dZ3 (RMSNorm backward)
+    f4 dz[8], z[8];
+    float q = 1.f;
+    {
+        const int64_t gi = valid ? (int64_t)a.gath_idx[row] : 0;
+        const float* dout = reinterpret_cast<const float*>(a.dout);
+        const float* gath = reinterpret_cast<const float*>(a.gath);
+        const float* zs = reinterpret_cast<const float*>(a.z_save);
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            dz[nt] = f4{0.f, 0.f, 0.f, 0.f};
+            z[nt] = f4{0.f, 0.f, 0.f, 0.f};
+            if (valid) {
+                dz[nt] = *reinterpret_cast<const f4*>(dout + row * a.dout_ld + n) +
+                         *reinterpret_cast<const f4*>(gath + gi * H + n);
+                z[nt] = *reinterpret_cast<const f4*>(zs + row * H + n);
+            }
+        }
+        if (valid) q = a.rden_save[row];
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+        const f4 s = ld4u(a.scale + 16 * nt + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dot += s[r] * dz[nt][r] * z[nt][r];
+    }
+    dot += __shfl_xor(dot, 16);
+    dot += __shfl_xor(dot, 32);
+    const float rms = q - RMS_EPS;
+    const float coef = rms > 0.f ? dot / (q * q * rms) * (a.dinv * a.dinv) : 0.f;
+    // scale partials: Σ over the wave's 16 rows (the lanes of one g) of dY ⊙ z / q, into LDS; the
+    // even wave of each pair adds its odd neighbour's behind the barrier (32 rows per partial)
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+        const f4 s = ld4u(a.scale + 16 * nt + 4 * g);
+        f4 dsc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float dy = dz[nt][r];
+            float v = dy * (z[nt][r] / q);
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            dsc[r] = v;
+            dz[nt][r] = s[r] * dy / q - z[nt][r] * coef;
+        }
+        if (ri == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * nt + 4 * g) = dsc;
+    }
+    f32c_stage_wait();
+    __syncthreads();
+    F32C_STAMP(0);
+    float* dz8 = reinterpret_cast<float*>(a.dz8);
+    const int64_t r8 = ((row >> 3) * H + 4 * g) * 8 + (row & 7);
+    if (!(wave & 1) && ri == 0) {
+        const int64_t p = (int64_t)blockIdx.x * (F32C_WAVES / 2) + (wave >> 1);
+        if (p < a.RP / 32) {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) {
+                const int n = 16 * nt + 4 * g;
+                *reinterpret_cast<f4*>(a.dscale_part + p * H + n) =
+                    *reinterpret_cast<const f4*>(red + wave * H + n) + *reinterpret_cast<const f4*>(red + (wave + 1) * H + n);
+            }
+        }
+    }
+    // ---- layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]; then de_in = dout + dZ_0 · W0a
+    f4 acc[8], dv[8];
+    const float* dout = reinterpret_cast<const float*>(a.dout);
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+        const int l = 3 - i;  // layer whose transposed weights this GEMM uses
+        if (i < 3) {
+            f32c_stage(wt + off[l - 1] + chain_image_off(H, l == 1 ? a.Kpack0 : H), (i & 1) ? img0 : img1);
+        } else {
+            // de_in = dout + dZ_0·W0a: dout lands during the last GEMM
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt)
+                dv[nt] = valid ? *reinterpret_cast<const f4*>(dout + row * a.dout_ld + 16 * nt + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        // dZ_l's R8 save is stored while it feeds the MFMAs
+        f32c_gemm(acc, dz, (i & 1) ? img1 : img0, lane, live ? dz8 + (int64_t)l * a.RP * H + r8 : nullptr);
+        F32C_STAMP(1);
+        if (i == 3) break;
+        // ReLU masks of hidden layer l-1: word nt*4 + r of the tile, bit = lane
+        const unsigned long long mine = l == 3 ? mw[2] : l == 2 ? mw[1] : mw[0];
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const unsigned long long wd = ((unsigned long long)__builtin_amdgcn_readlane((int)(mine >> 32), nt * 4 + r) << 32) |
+                                              (unsigned)__builtin_amdgcn_readlane((int)mine, nt * 4 + r);
+                dz[nt][r] = ((wd >> lane) & 1ull) && valid ? acc[nt][r] : 0.f;
+            }
+        F32C_STAMP(2);
+        f32c_stage_wait();
+        __syncthreads();
+        F32C_STAMP(3);
+    }
+    if (valid) {
+        // dZ_0 row-major for the node side (d(x·W0bᵀ)[v] = Σ_{dst(k)=v} dZ_0[k], likewise src), de_in
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            st4(reinterpret_cast<float*>(a.o2) + row * H + n, dz[nt]);
+            st4(reinterpret_cast<float*>(a.o1) + row * H + n, dv[nt] + acc[nt]);
+        }
+    }
+    F32C_STAMP(4);
+    F32C_STAMP_PRINT("f32b");
 }
 
 // --------------------------------------------------------------------------- host side
@@ -1688,6 +2053,24 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     a.z_save = sv->z;
     a.rden_save = sv->rden;
     a.ablate = ablate_mask();
+    if constexpr (sizeof(T) == 4 && H == 128 && MODE == MODE_EDGE) {
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        const SrcSeg& s0 = a.seg[0];
+        if (MGN_F32_CHAIN && a.L == 4 && a.has_norm && a.NOUT == H && a.nseg == 1 && !s0.idx &&
+            s0.dtype == MGN_F32 && s0.ncols == H && s0.coff == 0 && s0.ld % 4 == 0 && al16(s0.p) && a.K0 == H &&
+            a.Kpack0 == 3 * H && a.proj && al16(a.proj) && (!a.resid || al16(a.resid)) && al16(a.z_save) &&
+            al16(a.act8) && a.out_ld % 4 == 0 && ((uintptr_t)a.out & (out_dtype == MGN_F32 ? 15 : 7)) == 0 &&
+            !a.ablate) {
+            const int grid = (int)cdiv64(rows_pad(M), 16 * F32C_WAVES);
+            if (grid == 0) return 0;
+            const size_t lds = (2 * F32C_LAYER + 5 * H) * sizeof(float);
+            if (int e = set_lds((const void*)edge_fwd_f32_chain_kernel, lds)) return e;
+            ProfScope ps(PROF_FWD_EDGE, st);
+            hipLaunchKernelGGL(edge_fwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
+            MGN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     size_t r0 = (size_t)BM * (a.ldi > a.ldh ? a.ldi : a.ldh) * sizeof(T);
     const size_t zb = m->has_norm ? (size_t)BM * (H + 4) * sizeof(float) : 0;
     if (zb > r0) r0 = zb;
@@ -1750,6 +2133,21 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
     a.din_ld = o.din_ld;
     a.o1 = o.o1;
     a.o2 = o.o2;
+    if constexpr (sizeof(T) == 4 && H == 128 && MODE == MODE_EDGE) {
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        if (MGN_F32_CHAIN && a.L == 4 && a.has_norm && a.NOUT == H && a.Kpack0 == 3 * H && a.dout_dtype == MGN_F32 &&
+            a.dout_ld % 4 == 0 && al16(a.dout) && al16(a.gath) && a.gath_idx && al16(a.z_save) && al16(a.dz8) &&
+            al16(a.o1) && al16(a.o2) && al16(a.dscale_part) && BM == 32) {
+            const int grid = (int)cdiv64(a.RP, 16 * F32C_WAVES);
+            if (grid == 0) return 0;
+            const size_t lds = (2 * F32C_LAYER + F32C_WAVES * H) * sizeof(float);
+            if (int e = set_lds((const void*)edge_bwd_f32_chain_kernel, lds)) return e;
+            ProfScope ps(PROF_BWD_EDGE, st);
+            hipLaunchKernelGGL(edge_bwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
+            MGN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     const size_t lds = 2 * (size_t)BM * a.ldh * sizeof(T) + MGN_THREADS * 4 * sizeof(float);
     auto fn = mlp_bwd_kernel<T, H, BM, MODE>;
     if (int e = set_lds((const void*)fn, lds)) return e;

@@ -94,6 +94,9 @@ def test_host_size_functions(lib):
     # fragment-packed Linear: max(fwd, transposed) fragment count x 64 lanes x VEC
     assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_BF16) == max(8 * 12, 24 * 4) * 64 * 8
     assert lib.mgn_linear_pack_elems(2, 128, nat.MGN_F32) == max(1 * 32, 8 * 1) * 64
+    # fp32 128-wide Linears also carry the 128x128 chain image of the fp32 edge kernels
+    assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_F32) == max(8 * 96, 24 * 32) * 64 + 128 * 128
+    assert lib.mgn_linear_pack_elems(128, 100, nat.MGN_F32) == max(8 * 25, 8 * 32) * 64
     m = nat.Mlp()
     m.n_layers, m.in_dim, m.hidden, m.out_dim, m.has_norm, m.dtype = 4, 384, 128, 128, 1, nat.MGN_BF16
     ae, mw = ctypes.c_int64(), ctypes.c_int64()
