@@ -1630,7 +1630,12 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 #define F32C_STAMP(i)
 #define F32C_STAMP_PRINT(name)
 #endif
-constexpr int F32C_WAVES = 12;         // three waves per SIMD (168 VGPRs), 192 rows per workgroup
+#ifndef MGN_F32C_SB
+#define MGN_F32C_SB 0  // 1: single-buffered images, 6-wave workgroups, two workgroups per CU (A/B builds)
+#endif
+constexpr int F32C_WAVES = MGN_F32C_SB ? 6 : 12;  // three waves per SIMD (168 VGPRs), 16 rows per wave
+constexpr int F32C_NBUF = MGN_F32C_SB ? 1 : 2;    // LDS chain images per workgroup
+#define F32C_BOUNDS __launch_bounds__(F32C_WAVES * 64, 3)
 constexpr int F32C_LAYER = 128 * 128;  // floats per chain image (64 KiB)
 
 // The chain image of a pack region (fwd or transposed) of a fp32 [n][k] Linear, or NULL: it follows
@@ -1647,10 +1652,48 @@ __device__ __forceinline__ void f32c_stage(const float* __restrict__ src, float*
 }
 __device__ __forceinline__ void f32c_stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// 4x4 transpose inside each lane quad (lanes 4k..4k+3): lane i's v[r] <- lane r's v[i] (two DPP
+// butterfly stages: swap across lane bit 0, then bit 1). The moves are inline asm: with
+// __builtin_amdgcn_mov_dpp / update_dpp this ROCm 7.2 compiler folds the selects below into ONE DPP
+// move per stage (wrong values; an isolated 4-DPP kernel shows it); s_nop 1 covers the VALU-write ->
+// DPP-read hazard, which the compiler cannot see inside asm.
+__device__ __forceinline__ float dpp_xor1(float x) {
+    float r;
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ float dpp_xor2(float x) {
+    float r;
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ f4 quad_transpose(f4 v, int lane) {
+    f4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float p = dpp_xor1(v[r ^ 1]);
+        o[r] = ((r ^ lane) & 1) ? p : v[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float p = dpp_xor2(o[r ^ 2]);
+        v[r] = ((r ^ lane) & 2) ? p : o[r];
+    }
+    return v;
+}
+
+// The lane's address in a fp32 R8 save [rows/8][128][8] for the quad-transposed operand: lane (row, g)
+// holds column 16t + 4g + (row & 3) of rows (row & ~3) .. +3 after quad_transpose — 16 contiguous bytes,
+// and the 8 lanes of a row octet cover one 128-byte line (columns c..c+3 x 8 rows).
+__device__ __forceinline__ int64_t f32c_r8t(int64_t row, int g) {
+    return ((row >> 3) * 128 + 4 * g + (row & 3)) * 8 + (row & 4);
+}
+
 // acc[nt] += D^T tile nt of X·Wᵀ (16 rows) from the LDS image; x[t][r] = B operand of k-step (t, r).
-// save != NULL: also store the operand to its R8 save (save = the lane's R8 address of column 4(l>>4);
-// x[t][r] is column 16t + 4(l>>4) + r), four dwords per k-step group, spreading the saves over the
-// MFMAs (stored at once after each layer, every wave of the chip writes at the same time).
+// save != NULL: also store the operand to its R8 save (save = f32c_r8t of the lane; x[t][r] is column
+// 16t + 4(l>>4) + r of the lane's row): one quad-transposed 16-byte store per k-step group (full 128-byte
+// lines: 8 store instructions per layer instead of 32 partial-line dword stores), spread over the MFMAs
+// (stored at once after each layer, every wave of the chip writes at the same time).
 __device__ __forceinline__ void f32c_gemm(f4 (&acc)[8], const f4 (&x)[8], const float* img, int lane,
                                           float* save = nullptr) {
     // LDS reads run one half k-step group ahead (n-tiles 0..3, then 4..7: 16 MFMAs per half)
@@ -1672,19 +1715,16 @@ __device__ __forceinline__ void f32c_gemm(f4 (&acc)[8], const f4 (&x)[8], const 
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 acc[n0 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[h & 1][j][r], x[t][r], acc[n0 + j], 0, 0, 0);
-        if (save && (h & 1)) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) save[128 * t + 8 * r] = x[t][r];
-        }
+        if (save && (h & 1)) *reinterpret_cast<f4*>(save + 128 * t) = quad_transpose(x[t], lane);
     }
 }
 
-__global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(FwdArgs a) {
+__global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
     constexpr int H = 128;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* const img0 = reinterpret_cast<float*>(smem);
-    float* const img1 = img0 + F32C_LAYER;
-    float* const vec = img1 + F32C_LAYER;  // [5][H]: biases b0..b3, RMSNorm scale (LDS: no VMEM loads
+    float* const img1 = img0 + (F32C_NBUF - 1) * F32C_LAYER;
+    float* const vec = img0 + F32C_NBUF * F32C_LAYER;  // [5][H]: biases b0..b3, RMSNorm scale (LDS: no VMEM loads
                                            // behind the saves' stores, which would wait for them)
     const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15;
     const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + (threadIdx.x >> 6);
@@ -1695,26 +1735,27 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(Fwd
     const float* pk = reinterpret_cast<const float*>(a.wpack);
     f32c_stage(pk + chain_image_off(H, a.Kpack0), img0);  // layer 0: W0's e-column block
     pk += linear_pack_elems(H, a.Kpack0, MGN_F32);
-    int32_t pi = 0, pj = 0;
-    if (valid) {
-        pi = a.proj_i[row];
-        pj = a.proj_j[row];
-    }
+    // unconditional loads (rows past the end read the last row, then select 0): a conditional load
+    // compiles to a branch plus a full wait, eight of them in a row for the gathers
+    const int64_t rowc = valid ? row : a.M - 1;
+    const int32_t pi = a.proj_i[rowc], pj = a.proj_j[rowc];
     const float* e = reinterpret_cast<const float*>(a.seg[0].p);
     f4 x[8], acc[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
-        x[t] = valid ? *reinterpret_cast<const f4*>(e + row * a.seg[0].ld + 16 * t + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 8; ++t) x[t] = *reinterpret_cast<const f4*>(e + rowc * a.seg[0].ld + 16 * t + 4 * g);
     // layer 0's accumulator starts at P_i + P_j + b0: [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]
     {
         const f4* ppi = reinterpret_cast<const f4*>(a.proj + (int64_t)pi * (2 * H)) + g;
         const f4* ppj = reinterpret_cast<const f4*>(a.proj + (int64_t)pj * (2 * H) + H) + g;
 #pragma unroll
-        for (int nt = 0; nt < 8; ++nt) acc[nt] = valid ? ppi[4 * nt] : f4{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = ppi[4 * nt];
         __builtin_amdgcn_sched_barrier(0);  // two passes: 32 registers of gathers in flight, not 64
 #pragma unroll
-        for (int nt = 0; nt < 8; ++nt)
-            if (valid) acc[nt] += ppj[4 * nt];
+        for (int nt = 0; nt < 8; ++nt) acc[nt] += ppj[4 * nt];
+    }
+    if (!valid) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) x[t] = acc[t] = f4{0.f, 0.f, 0.f, 0.f};
     }
     for (int i = threadIdx.x; i < 5 * H; i += F32C_WAVES * 64) {
         const int vl = i >> 7;
@@ -1727,15 +1768,17 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(Fwd
     for (int nt = 0; nt < 8; ++nt) acc[nt] += *reinterpret_cast<const f4*>(vec + 16 * nt + 4 * g);
     F32C_STAMP(0);
     float* act = reinterpret_cast<float*>(a.act8);
-    const int64_t r8 = ((row >> 3) * H + 4 * g) * 8 + (row & 7);  // R8 index of (row, 4g)
+    const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
     const float* res = reinterpret_cast<const float*>(a.resid);
     f4 rv[8];
 #pragma unroll 1
     for (int l = 0; l < 4; ++l) {
+        const float* nxt = nullptr;
         if (l < 3) {
             // layer l+1's image streams into the other buffer during this layer's MFMAs (its readers,
-            // layer l-1, passed the last barrier)
-            f32c_stage(pk + chain_image_off(H, H), (l & 1) ? img0 : img1);
+            // layer l-1, passed the last barrier); single-buffered: after every wave's MFMAs
+            nxt = pk + chain_image_off(H, H);
+            if (F32C_NBUF == 2) f32c_stage(nxt, (l & 1) ? img0 : img1);
             pk += linear_pack_elems(H, H, MGN_F32);
         } else {
             // the residual lands during the last GEMM
@@ -1765,6 +1808,10 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(Fwd
             // the tile's 32 ballot words of layer l: word nt*4 + r from lane nt*4 + r
             if (live && lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
             F32C_STAMP(2);
+            if (F32C_NBUF == 1) {
+                __syncthreads();
+                f32c_stage(nxt, img0);
+            }
             f32c_stage_wait();
             __syncthreads();
             F32C_STAMP(3);
@@ -1805,12 +1852,12 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_fwd_f32_chain_kernel(Fwd
 // chains exactly like the forward with the transposed chain images. Outputs match mlp_bwd_kernel: dZ_l
 // R8 saves, dZ_0 row-major, de_in = dout + dZ_0·W0a, and RMSNorm-scale partials per 32 rows (the
 // generic kernel's partial count: two waves combine in LDS).
-__global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(BwdArgs a) {
+__global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
     constexpr int H = 128;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* const img0 = reinterpret_cast<float*>(smem);
-    float* const img1 = img0 + F32C_LAYER;
-    float* const red = img1 + F32C_LAYER;  // [F32C_WAVES][H] per-wave RMSNorm-scale partials
+    float* const img1 = img0 + (F32C_NBUF - 1) * F32C_LAYER;
+    float* const red = img0 + F32C_NBUF * F32C_LAYER;  // [F32C_WAVES][H] per-wave RMSNorm-scale partials
     const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15, wave = threadIdx.x >> 6;
     const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + wave;
     const int64_t row0 = tile * 16, row = row0 + ri;
@@ -1838,22 +1885,28 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(Bwd
     f4 dz[8], z[8];
     float q = 1.f;
     {
-        const int64_t gi = valid ? (int64_t)a.gath_idx[row] : 0;
+        // unconditional loads of the last row for rows past the end (then 0): see the forward
+        const int64_t rowc = valid ? row : a.M - 1;
+        const int64_t gi = a.gath_idx[rowc];
         const float* dout = reinterpret_cast<const float*>(a.dout);
         const float* gath = reinterpret_cast<const float*>(a.gath);
         const float* zs = reinterpret_cast<const float*>(a.z_save);
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) {
             const int n = 16 * nt + 4 * g;
-            dz[nt] = f4{0.f, 0.f, 0.f, 0.f};
-            z[nt] = f4{0.f, 0.f, 0.f, 0.f};
-            if (valid) {
-                dz[nt] = *reinterpret_cast<const f4*>(dout + row * a.dout_ld + n) +
-                         *reinterpret_cast<const f4*>(gath + gi * H + n);
-                z[nt] = *reinterpret_cast<const f4*>(zs + row * H + n);
-            }
+            dz[nt] = *reinterpret_cast<const f4*>(dout + rowc * a.dout_ld + n);
+            z[nt] = *reinterpret_cast<const f4*>(zs + rowc * H + n);
         }
-        if (valid) q = a.rden_save[row];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) dz[nt] += *reinterpret_cast<const f4*>(gath + gi * H + 16 * nt + 4 * g);
+        const float qv = a.rden_save[rowc];
+        if (valid) {
+            q = qv;
+        } else {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) dz[nt] = z[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        }
     }
     float dot = 0.f;
 #pragma unroll
@@ -1889,7 +1942,7 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(Bwd
     __syncthreads();
     F32C_STAMP(0);
     float* dz8 = reinterpret_cast<float*>(a.dz8);
-    const int64_t r8 = ((row >> 3) * H + 4 * g) * 8 + (row & 7);
+    const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
     if (!(wave & 1) && ri == 0) {
         const int64_t p = (int64_t)blockIdx.x * (F32C_WAVES / 2) + (wave >> 1);
         if (p < a.RP / 32) {
@@ -1907,8 +1960,10 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(Bwd
 #pragma unroll 1
     for (int i = 0; i < 4; ++i) {
         const int l = 3 - i;  // layer whose transposed weights this GEMM uses
+        const float* nxt = nullptr;
         if (i < 3) {
-            f32c_stage(wt + off[l - 1] + chain_image_off(H, l == 1 ? a.Kpack0 : H), (i & 1) ? img0 : img1);
+            nxt = wt + off[l - 1] + chain_image_off(H, l == 1 ? a.Kpack0 : H);
+            if (F32C_NBUF == 2) f32c_stage(nxt, (i & 1) ? img0 : img1);
         } else {
             // de_in = dout + dZ_0·W0a: dout lands during the last GEMM
 #pragma unroll
@@ -1932,6 +1987,10 @@ __global__ __launch_bounds__(F32C_WAVES * 64) void edge_bwd_f32_chain_kernel(Bwd
                 dz[nt][r] = ((wd >> lane) & 1ull) && valid ? acc[nt][r] : 0.f;
             }
         F32C_STAMP(2);
+        if (F32C_NBUF == 1) {
+            __syncthreads();
+            f32c_stage(nxt, img0);
+        }
         f32c_stage_wait();
         __syncthreads();
         F32C_STAMP(3);
@@ -2063,7 +2122,7 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
             !a.ablate) {
             const int grid = (int)cdiv64(rows_pad(M), 16 * F32C_WAVES);
             if (grid == 0) return 0;
-            const size_t lds = (2 * F32C_LAYER + 5 * H) * sizeof(float);
+            const size_t lds = (F32C_NBUF * F32C_LAYER + 5 * H) * sizeof(float);
             if (int e = set_lds((const void*)edge_fwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_FWD_EDGE, st);
             hipLaunchKernelGGL(edge_fwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
@@ -2140,7 +2199,7 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
             al16(a.o1) && al16(a.o2) && al16(a.dscale_part) && BM == 32) {
             const int grid = (int)cdiv64(a.RP, 16 * F32C_WAVES);
             if (grid == 0) return 0;
-            const size_t lds = (2 * F32C_LAYER + F32C_WAVES * H) * sizeof(float);
+            const size_t lds = (F32C_NBUF * F32C_LAYER + F32C_WAVES * H) * sizeof(float);
             if (int e = set_lds((const void*)edge_bwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_BWD_EDGE, st);
             hipLaunchKernelGGL(edge_bwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
@@ -2723,6 +2782,9 @@ __global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
     }
 }
 
+#ifndef MGN_COMB_PAIR
+#define MGN_COMB_PAIR 0  // 1: node_grad's segment-sum items two at a time (A/B builds)
+#endif
 struct CombArgs {
     const void* dz0;      // [E][H] (T) dZ of the edge layer 0, target-sorted edges
     const int32_t* col_ptr;
@@ -2764,6 +2826,83 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
             kes[j] = ptr[v + 1];
         }
     }
+#if MGN_COMB_PAIR
+    // two items at a time: the first edge group of BOTH items is in flight together (one round trip
+    // for the common in-degree <= SG), longer segments finish item by item; same sums in edge order
+    auto item = [&](int j, int& s, int& r, int& c) {
+        const int it = threadIdx.x + j * MGN_THREADS;
+        s = it / (BM * CPR);
+        const int rem = it - s * (BM * CPR);
+        r = rem / CPR;
+        c = (rem - r * CPR) * CH;
+        return it < 2 * BM * CPR;
+    };
+    auto group = [&](int s, int c, int k, int ke, float (&acc)[CH]) {
+        int64_t src[SG];
+#pragma unroll
+        for (int u = 0; u < SG; ++u) {
+            const int ku = k + u < ke ? k + u : ke - 1;
+            src[u] = s == 0 ? (int64_t)ku : (int64_t)a.row_perm[ku];
+        }
+        float t[SG][CH];
+#pragma unroll
+        for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
+#pragma unroll
+        for (int u = 0; u < SG; ++u)
+            if (k + u < ke) {
+#pragma unroll
+                for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
+            }
+    };
+#pragma unroll 1
+    for (int j = 0; j < NIT; j += 2) {
+        int s0, r0, c0, s1 = 0, r1 = 0, c1 = 0;
+        if (!item(j, s0, r0, c0)) break;
+        const bool two = j + 1 < NIT && item(j + 1, s1, r1, c1);
+        const int kb0 = kbs[j], ke0 = kes[j];
+        const int kb1 = two ? kbs[j + 1] : 0, ke1 = two ? kes[j + 1] : 0;
+        float acc0[CH], acc1[CH];
+#pragma unroll
+        for (int e = 0; e < CH; ++e) acc0[e] = acc1[e] = 0.f;
+        if (kb0 < ke0 && kb1 < ke1) {
+            // both first groups' loads issued before either's adds
+            int64_t sa[SG], sb[SG];
+#pragma unroll
+            for (int u = 0; u < SG; ++u) {
+                const int ka = kb0 + u < ke0 ? kb0 + u : ke0 - 1, kq = kb1 + u < ke1 ? kb1 + u : ke1 - 1;
+                sa[u] = s0 == 0 ? (int64_t)ka : (int64_t)a.row_perm[ka];
+                sb[u] = s1 == 0 ? (int64_t)kq : (int64_t)a.row_perm[kq];
+            }
+            float ta[SG][CH], tb[SG][CH];
+#pragma unroll
+            for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + sa[u] * H + c0, ta[u]);
+#pragma unroll
+            for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + sb[u] * H + c1, tb[u]);
+#pragma unroll
+            for (int u = 0; u < SG; ++u) {
+                if (kb0 + u < ke0) {
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) acc0[e] += ta[u][e];
+                }
+                if (kb1 + u < ke1) {
+#pragma unroll
+                    for (int e = 0; e < CH; ++e) acc1[e] += tb[u][e];
+                }
+            }
+#pragma unroll 1
+            for (int k = kb0 + SG; k < ke0; k += SG) group(s0, c0, k, ke0, acc0);
+#pragma unroll 1
+            for (int k = kb1 + SG; k < ke1; k += SG) group(s1, c1, k, ke1, acc1);
+        } else {
+#pragma unroll 1
+            for (int k = kb0; k < ke0; k += SG) group(s0, c0, k, ke0, acc0);
+#pragma unroll 1
+            for (int k = kb1; k < ke1; k += SG) group(s1, c1, k, ke1, acc1);
+        }
+        Chunk<T>::store(B + (size_t)r0 * a.ldb + s0 * a.HP + c0, acc0);
+        if (two) Chunk<T>::store(B + (size_t)r1 * a.ldb + s1 * a.HP + c1, acc1);
+    }
+#else
 #pragma unroll 1
     for (int j = 0; j < NIT; ++j) {
         const int it = threadIdx.x + j * MGN_THREADS;
@@ -2794,6 +2933,7 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
         }
         Chunk<T>::store(B + (size_t)r * a.ldb + s * a.HP + c, acc);
     }
+#endif
     const int padc = a.HP - H;
     if (padc > 0)
         for (int it = threadIdx.x; it < 2 * BM * padc; it += MGN_THREADS) {

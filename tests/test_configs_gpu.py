@@ -24,6 +24,7 @@ import pytest
 import torch
 
 from oracle import mgn_oracle as O
+from _orders import assert_vs_truth_orders, order_spread
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -41,11 +42,6 @@ def _built():
 def relerr(a, b):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
-
-
-def assert_vs_truth(got, ref32, ref64, floor=1e-5, tie_tol=2e-3, what=""):
-    e_ref, e_got = relerr(ref32, ref64), relerr(got, ref64)
-    assert e_got <= max(floor, 2 * e_ref, tie_tol), f"{what}: libmgn {e_got:.2e} vs fp64, reference fp32 {e_ref:.2e}"
 
 
 def assert_close_elem(got, ref, tol=1e-5):
@@ -139,8 +135,11 @@ def test_plate_simulator_train_step_vs_oracle(plate, dtype, mp, h):
         assert relerr(net, yr) < 1e-4
         assert relerr(net, y64) <= max(1e-6, 2 * relerr(yr, y64))
         assert abs(loss.item() - lr.item()) <= 1e-4 * lr.item()
+        sp = order_spread(lambda q, i: O.l2_loss(tdn_r, O.encode_process_decode(i["x"], ei, i["ea"], q, mp), nt), rp,
+                          {k: v.grad for k, v in p64.items()}, n_orders=24,
+                          inputs={"x": (nfn_r, "nodes_encoder.0.weight"), "ea": (ean_r, "edges_encoder.0.weight")})
         for k, p in sim.model.named_parameters():
-            assert_vs_truth(p.grad, rp[k].grad, p64[k].grad, what=k)
+            assert_vs_truth_orders(p.grad, rp[k].grad, p64[k].grad, sp[k], what=k)
         return
     pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
     with torch.autocast("cpu", dtype=torch.bfloat16):
