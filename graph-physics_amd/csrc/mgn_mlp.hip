@@ -1682,6 +1682,26 @@ __device__ __forceinline__ f4 quad_transpose(f4 v, int lane) {
     return v;
 }
 
+#ifndef MGN_F32C_DPPRED
+#define MGN_F32C_DPPRED 1  // 0: the fp32 backward's RMSNorm-scale row sums on LDS-crossbar shuffles (A/B builds)
+#endif
+// the 4 components of v summed over the 16 lanes of a DPP row (as mgn_chain16.hip's row16_sum4):
+// lane m returns component 2(m&1) + ((m>>1)&1); pairs m^1 trade two components, pairs m^2 one, then
+// rotations by 4 and 8 add the four lanes holding the same component
+__device__ __forceinline__ float f32c_row16_sum4(const f4& v, int m) {
+    const bool odd = m & 1, b1 = (m >> 1) & 1;
+    const float s0 = odd ? v[0] : v[2], s1 = odd ? v[1] : v[3];
+    float k0 = odd ? v[2] : v[0], k1 = odd ? v[3] : v[1];
+    k0 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xF, 0xF, false));
+    k1 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xF, 0xF, false));
+    const float sb = b1 ? k0 : k1;
+    float k = b1 ? k1 : k0;
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(sb), 0x4E, 0xF, 0xF, false));
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(k), 0x124, 0xF, 0xF, false));  // row_ror:4
+    k += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(k), 0x128, 0xF, 0xF, false));  // row_ror:8
+    return k;
+}
+
 // The lane's address in a fp32 R8 save [rows/8][128][8] for the quad-transposed operand: lane (row, g)
 // holds column 16t + 4g + (row & 3) of rows (row & ~3) .. +3 after quad_transpose — 16 contiguous bytes,
 // and the 8 lanes of a row octet cover one 128-byte line (columns c..c+3 x 8 rows).
@@ -1921,6 +1941,11 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
     const float coef = rms > 0.f ? dot / (q * q * rms) * (a.dinv * a.dinv) : 0.f;
     // scale partials: Σ over the wave's 16 rows (the lanes of one g) of dY ⊙ z / q, into LDS; the
     // even wave of each pair adds its odd neighbour's behind the barrier (32 rows per partial)
+#if MGN_F32C_DPPRED
+    // transposing DPP row sums (6 DPP adds for the 4 components instead of 16 LDS-crossbar shuffles):
+    // lane ri < 4 ends with component 2(ri&1) + ((ri>>1)&1) summed over the row
+    const int r4 = 2 * (ri & 1) + ((ri >> 1) & 1);
+#endif
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
         const f4 s = ld4u(a.scale + 16 * nt + 4 * g);
@@ -1929,14 +1954,21 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
         for (int r = 0; r < 4; ++r) {
             const float dy = dz[nt][r];
             float v = dy * (z[nt][r] / q);
+#if !MGN_F32C_DPPRED
             v += __shfl_xor(v, 1);
             v += __shfl_xor(v, 2);
             v += __shfl_xor(v, 4);
             v += __shfl_xor(v, 8);
+#endif
             dsc[r] = v;
             dz[nt][r] = s[r] * dy / q - z[nt][r] * coef;
         }
+#if MGN_F32C_DPPRED
+        const float dsum = f32c_row16_sum4(dsc, ri);
+        if (ri < 4) red[wave * H + 16 * nt + 4 * g + r4] = dsum;
+#else
         if (ri == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * nt + 4 * g) = dsc;
+#endif
     }
     f32c_stage_wait();
     __syncthreads();
