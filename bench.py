@@ -44,9 +44,9 @@ def parse():
     ap.add_argument("--mp", type=int, default=15)
     ap.add_argument("--hidden", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-steps", type=int, default=3,
-                    help="timed CPU baseline steps after one warm-up step: a bounded sample (~30 s on 16 cores) "
-                         "of the same workload, median reported (0: skip)")
+    ap.add_argument("--cpu-steps", type=int, default=10,
+                    help="timed CPU baseline steps after 3 warm-up steps (SURVEY §8(d): >= 10 timed, 3 warm-up; "
+                         "a bounded sample, ~100 s on 16 cores) of the same workload, median reported (0: skip)")
     ap.add_argument("--sustain", type=float, default=5.0,
                     help="seconds of further replayed steps after the timed K (reported as `sustained`)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -123,25 +123,39 @@ def make_workload(a, dev, rank, mesh):
         "reference aneurysm mock mesh (k-hop 2 built on device), synthetic node features"
 
 
-def class_work(n, e, h, mp, lay, nparams, nweights, es):
-    """Algorithmic work per STEP of every kernel class (SURVEY.md §8(a,d) per-unit figures x the units
-    the class processes; the reference algorithm's FLOPs, so the split-layer-0 reformulation is not
-    credited with work it skips): ("mfma", FLOPs) or ("hbm", bytes).
-      edge MLP 12h²/edge fwd (a2): fwd_edge does the e block of layer 0 + the 3 hidden Linears (8h²),
-      the x_i / x_j blocks of layer 0 (4h²/edge, applied per node) run in proj for block 0 and inside
-      the previous block's node-MLP forward for blocks 1.. (ABI v8 hand-off); backward data the same split
-      (bwd_edge 8h², combine 4h²); weight gradients 12h²/edge + 10h²/node in one ring launch; node MLP
-      10h²/node (a3); encoders/decoder 2(in·h + 3h²) per row and 2(3h² + h·out) (a7).
-      AdamW: p, g, m, v read + p, m, v written (28 B/param); pack: fp32 weights in, 2 bf16 copies out."""
+def class_work(n, e, h, mp, lay, nparams, nweights, es, launches=None):
+    """Work per STEP of every kernel class: {class: (bound, executed, algorithmic)}, FLOPs for "mfma"
+    classes, bytes for "hbm" ones (SURVEY.md §8(a,d) per-unit figures x the units the class processes).
+    `executed` is what the class's kernels compute: the per-class `frac` uses it, so no class is credited
+    with work another class (or no kernel) does. `algorithmic` is the reference algorithm's work the
+    class stands for (§8(d)): reported beside the executed figure for the dominant class only.
+      edge layer 0 is split: fwd_edge runs the e block + 3 hidden Linears (8h²/edge); the
+      x_i / x_j blocks become node projections, 4h²/NODE, in `proj` (one launch per block on the
+      generic path, block 0 only on the chained bf16 path) or inside the previous block's node-MLP
+      forward (chained hand-off); bwd_edge 8h²/edge; combine (node_grad) dx += [dP_i‖dP_j]·W0[:, h:3h]ᵀ,
+      4h²/node; node MLP 10h²/node fwd and bwd; weight gradients (ring, or the generic kernel on the
+      generic path) 8h²/edge + 14h²/node executed vs the reference's 12h²/edge + 10h²/node;
+      encoders/decoder 2(in·h + 3h²) per row fwd and weight gradients, backward data 6h² per encoder
+      row (no input gradient) + the decoder's 2(3h² + h·out). AdamW: p, g, m, v read + p, m, v
+      written (28 B/param); pack: fp32 weights in, 2 bf16 copies out."""
+    launches = launches or {}
     enc = 2 * (lay["edge_in"] * h + 3 * h * h) * e + 2 * (lay["node_in"] * h + 3 * h * h) * n
     dec = 2 * (3 * h * h + h * lay["out"]) * n
+    nproj = launches.get("proj", mp)  # projection launches per step
+    handoff = max(mp - nproj, 0)      # blocks whose projections run inside the previous node-MLP forward
+    wg_exec, wg_alg = mp * (8 * h * h * e + 14 * h * h * n), mp * (12 * h * h * e + 10 * h * h * n)
     return {
-        "fwd_edge": ("mfma", mp * 8 * h * h * e), "proj": ("mfma", min(mp, 1) * 4 * h * h * e),
-        "fwd_node": ("mfma", mp * 10 * h * h * n + max(mp - 1, 0) * 4 * h * h * e), "bwd_edge": ("mfma", mp * 8 * h * h * e),
-        "combine": ("mfma", mp * 4 * h * h * e), "bwd_node": ("mfma", mp * 10 * h * h * n),
-        "wgrad": ("mfma", mp * (12 * h * h * e + 10 * h * h * n)),
-        "fwd_dense": ("mfma", enc + dec), "bwd_dense": ("mfma", enc + dec), "wgrad_dense": ("mfma", enc + dec),
-        "adamw": ("hbm", 28 * nparams), "pack": ("hbm", 8 * nweights),
+        "fwd_edge": ("mfma", mp * 8 * h * h * e, mp * 12 * h * h * e),
+        "proj": ("mfma", nproj * 4 * h * h * n, None),
+        "fwd_node": ("mfma", mp * 10 * h * h * n + handoff * 4 * h * h * n, mp * 10 * h * h * n),
+        "bwd_edge": ("mfma", mp * 8 * h * h * e, mp * 12 * h * h * e),
+        "combine": ("mfma", mp * 4 * h * h * n, None),
+        "bwd_node": ("mfma", mp * 10 * h * h * n, mp * 10 * h * h * n),
+        "wgrad": ("mfma", wg_exec, wg_alg),
+        "fwd_dense": ("mfma", enc + dec, enc + dec),
+        "bwd_dense": ("mfma", 6 * h * h * (e + n) + dec, enc + dec),
+        "wgrad_dense": ("mfma", enc + dec, enc + dec),
+        "adamw": ("hbm", 28 * nparams, 28 * nparams), "pack": ("hbm", 8 * nweights, 8 * nweights),
     }
 
 
@@ -238,24 +252,28 @@ def analyse(a, prof, sim, lay, N, E, dt):
     es = 2 if a.dtype == "bf16" else 4
     nparams = sum(p.numel() for p in sim.parameters())
     nweights = sum(m.weight.numel() for m in sim.model.modules() if isinstance(m, torch.nn.Linear))
-    work = class_work(N, E, h, a.mp, lay, nparams, nweights, es)
+    per_step = {k: cnt / a.steps for k, (ms, cnt) in prof.items() if cnt}
+    work = class_work(N, E, h, a.mp, lay, nparams, nweights, es, per_step)
     if not prof.get("wgrad", (0, 0))[1] and prof.get("wgrad_dense", (0, 0))[1]:
-        # no ring launches (fp32, or h != 128): every weight gradient, the processor blocks' too,
-        # runs on the generic kernel the profiler files under wgrad_dense
-        work["wgrad_dense"] = ("mfma", work["wgrad_dense"][1] + work["wgrad"][1])
+        # no ring launches (the generic path): every weight gradient, the processor blocks' too, runs
+        # on the generic kernel the profiler files under wgrad_dense
+        w, d = work["wgrad"], work["wgrad_dense"]
+        work["wgrad_dense"] = ("mfma", w[1] + d[1], w[2] + d[2])
     kinds = {}
     for k, (ms, cnt) in prof.items():
         if cnt:
             kinds[k] = {"total_ms": round(ms, 4), "launches": cnt, "avg_us": round(1000 * ms / cnt, 2),
                         "ms_per_step": round(ms / a.steps, 4)}
             if k in work:
-                bound, amount = work[k]
+                bound, amount = work[k][:2]
                 per_s = amount * a.steps / (ms / 1000)
                 if bound == "mfma":
                     kinds[k].update(bound="mfma", tflops=round(per_s / 1e12, 2),
                                     frac=round(per_s / 1e12 / PEAK[a.dtype], 4))
                 else:
                     kinds[k].update(bound="hbm", gbs=round(per_s / 1e9, 1), frac=round(per_s / 1e9 / HBM_PEAK, 4))
+                if kinds[k]["frac"] > 1.0:  # executed work above peak would be a crediting bug: flagged, not hidden
+                    kinds[k]["error"] = "frac above peak: executed-work credit is wrong for this class"
     roof = None
     wl = workload_key(a)
     step_flops = 3 * (a.mp * (12 * h * h * E + 10 * h * h * N) + 2 * (lay["edge_in"] * h + 3 * h * h) * E
@@ -276,17 +294,25 @@ def analyse(a, prof, sim, lay, N, E, dt):
             dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
             picked = "eager HIP-event profile (no replay trace recorded for these sources and workload)"
         kd = kinds[dom]
-        bound, amount = work.get(dom, ("mfma", 0))
-        per_launch = amount * a.steps / kd["launches"]
+        bound, executed, algorithmic = work.get(dom, ("mfma", 0, None))
+        credit = algorithmic if algorithmic is not None else executed
+        per_launch = credit * a.steps / kd["launches"]
+        per_launch_x = executed * a.steps / kd["launches"]
         avg_s = kd["total_ms"] / 1000 / kd["launches"]
-        ach = per_launch / avg_s / (1e12 if bound == "mfma" else 1e9)
+        scale = 1e12 if bound == "mfma" else 1e9
+        ach, ach_x = per_launch / avg_s / scale, per_launch_x / avg_s / scale
         peak = PEAK[a.dtype] if bound == "mfma" else HBM_PEAK
         pmc = pmc_lookup(dom, wl)
+        unit = "flops" if bound == "mfma" else "bytes"
         roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak,
                 "unit": "TFLOP/s" if bound == "mfma" else "GB/s", "frac": round(ach / peak, 4),
+                "credit": "algorithmic (SURVEY §8(d): the reference algorithm's work this kernel class stands for)"
+                          if algorithmic is not None else "executed",
+                "executed": {unit + "_per_launch": per_launch_x, "achieved": round(ach_x, 2),
+                             "frac": round(ach_x / peak, 4)},
                 "traffic": pmc.get("hbm_bytes"), "traffic_source": pmc.get("source"),
                 "mfma_util_measured": pmc.get("mfma_util"), "dominant_from": picked,
-                ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per_launch,
+                unit + "_per_launch": per_launch,
                 "avg_launch_us": round(avg_s * 1e6, 2), "launches_per_step": kd["launches"] / a.steps,
                 "peak_source": "MI355X_MICROARCH.md: dense bf16 MFMA 2.5 PFLOP/s (fp32 MFMA 157.3), HBM3E 8 TB/s",
                 "step": {"tflops_per_s": round(step_tf, 2), "frac": round(step_tf / PEAK[a.dtype], 4),
@@ -422,10 +448,31 @@ def main():
         sus = {"steps": n_s, "seconds": round(ds, 3), "value": round(world * n_s / ds, 3), "unit": "steps/s"}
         log("sustained: %d steps in %.2f s" % (n_s, ds))
     prof = profile_classes(a, step) if not a.no_profile else {}
+    nparams = sum(p.numel() for p in sim.parameters())
+    dp_info = None
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+        # every rank ran the same configuration: world size, parameter count, and (overlapped
+        # all-reduce) gradient buckets that covered every parameter exactly once
+        covered = step.buckets.covered if (step.overlap and step.buckets is not None) else -1
+        if covered >= 0 and covered != nparams:
+            raise RuntimeError("gradient buckets covered %d of %d parameters" % (covered, nparams))
+        chk = torch.tensor([dist.get_world_size(), nparams, covered, a.batch, a.mp, a.hidden],
+                           device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.int64)
+        allc = [torch.empty_like(chk) for _ in range(world)]
+        dist.all_gather(allc, chk)
+        if any(not torch.equal(c, chk) for c in allc):
+            raise RuntimeError("ranks disagree on (world, params, covered, batch, mp, hidden): %s"
+                               % [c.tolist() for c in allc])
+        stats = getattr(sim, "_stats_buf", None)
+        dp_info = {"world_size": dist.get_world_size(), "world_size_agreed_by_all_ranks": True,
+                   "grad_allreduce_bytes_per_step": 4 * nparams,
+                   "stats_allreduce_bytes_per_step": 4 * stats.numel() if stats is not None else None,
+                   "grad_buckets_cover_all_params": covered == nparams if covered >= 0 else None,
+                   "grad_buckets_per_step": step.buckets.issued if (step.overlap and step.buckets) else None,
+                   "backend": dist.get_backend()}
     last_loss = float(loss.item())
 
     if rank != 0:
@@ -435,9 +482,16 @@ def main():
         return
 
     kinds, roof = analyse(a, prof, sim, lay, N, E, dt)
+    # value: per-GPU training steps (one batch of a.batch graphs each) completed by ALL ranks per second
+    # (whole-job aggregate, weak scaling). With N ranks one optimizer step consumes N such batches:
+    # the optimizer-step rate and the graph rate are reported separately.
     value = world * a.steps / dt
+    gpb = a.batch if a.workload == "cylinder" else 1
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "steps/s", "n_gpus": world, "steps": a.steps,
+        "value_definition": "per-GPU training steps (batch of %d graphs) of all %d rank(s) per second; "
+                            "= optimizer_steps_per_s x n_gpus" % (gpb, world),
+        "optimizer_steps_per_s": round(a.steps / dt, 3), "graphs_per_s": round(value * gpb, 2),
         "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
         "data": "synthetic: %s, random-init weights (seed 0)" % datadesc,
@@ -451,9 +505,11 @@ def main():
         "config": {"workload": workload, "nodes_per_gpu": N, "edges_per_gpu": E,
                    "global_batch": (a.batch if a.workload == "cylinder" else 1) * world,
                    "parallelism": "dp%d" % world,
-                   "graphs_per_sec": round(value * (a.batch if a.workload == "cylinder" else 1), 2)},
+                   "graphs_per_sec": round(value * gpb, 2)},
         "roofline": roof, "kernels": kinds, "last_loss": last_loss,
     }
+    if dp_info is not None:
+        out["data_parallel"] = dp_info
     if sus is not None:
         out["sustained"] = sus
 
@@ -481,6 +537,11 @@ def main():
         sec["cfgC_plate"] = secondary(a, dev, mesh, "Config C: DeformingPlate MGN at plate.json's sizes (MP=10, h=64, "
                                       "bf16), world edges + relative-position features, 1 graph",
                                       dtype="bf16", mp=10, hidden=64, batch=1, workload="plate")
+        # BASELINE config 4 per GPU (Cfg E): the reference's aneurysm mesh, k-hop 2 built on device
+        # (N=22,535, E=1,395,256), MP=15, h=128, bf16 — the largest single-GPU workload
+        sec["cfgE_aneurysm"] = secondary(a, dev, mesh, "Config E per GPU: 3D-CoarseAneurysm, k-hop 2 (1 graph, "
+                                         "N=22,535, E=1,395,256), MP=15, h=128, bf16", dtype="bf16", mp=15,
+                                         hidden=128, batch=1, workload="aneurysm")
         out["secondary"] = sec
     print(json.dumps(out), flush=True)
     if world > 1:
@@ -567,7 +628,7 @@ def one_step_mse(sim, mesh, dev, a):
             "frames": "3->4, 4->5 (held out), B=1, weights after the timed steps"}
 
 
-def cpu_baseline(a, b, lay, warmup=1):
+def cpu_baseline(a, b, lay, warmup=3):
     """The reference algorithm on the host (oracle = op-for-op restatement of the reference's
     PyTorch CPU path, pinned to golden vectors), same workload, fp32, all cores: `warmup` untimed
     steps, then a.cpu_steps timed ones, median."""

@@ -145,13 +145,16 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         const double* __restrict__ hyper, double beta1,
-                                                        double beta2, double eps, double wd, unsigned* err) {
+                                                        double beta2, double eps, double wd, unsigned* err,
+                                                        int count_skip) {
 #pragma clang fp contract(off)
     if (err) {  // a pending validation error: the reference raised before its optimizer step
         const unsigned e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e & MGN_ERR_ANY) {
             if (blockIdx.x == 0 && threadIdx.x == 0) {
-                if ((e & MGN_ERR_SKIP_MASK) != MGN_ERR_SKIP_MASK) atomicAdd(err, MGN_ERR_SKIP_ONE);
+                // one count per optimizer STEP: of a step's launches (one per parameter group /
+                // parameter) only the first has count_skip set (mgn_adamw_dev2)
+                if (count_skip && (e & MGN_ERR_SKIP_MASK) != MGN_ERR_SKIP_MASK) atomicAdd(err, MGN_ERR_SKIP_ONE);
                 atomicOr(err, MGN_ERR_STALE);
             }
             return;
@@ -527,17 +530,25 @@ __global__ __launch_bounds__(256) void masked_mse_bwd(const float* __restrict__ 
 
 extern "C" {
 
-int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                  const double* hyper, double beta1, double beta2, double eps, double weight_decay,
-                  uint32_t* err_word, mgn_stream_t stream) {
+int mgn_adamw_dev2(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
+                   uint32_t* err_word, int32_t count_skip, mgn_stream_t stream) {
     if (n == 0) return 0;
     int64_t blocks = cdiv64(cdiv64(n, 4), 256);
     if (blocks > 512) blocks = 512;
     ProfScope ps(PROF_ADAMW, (hipStream_t)stream);
     hipLaunchKernelGGL(adamw_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, param, grad,
-                       exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay, (unsigned*)err_word);
+                       exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay, (unsigned*)err_word,
+                       (int)(count_skip != 0));
     MGN_LAUNCH_CHECK();
     return 0;
+}
+
+int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  const double* hyper, double beta1, double beta2, double eps, double weight_decay,
+                  uint32_t* err_word, mgn_stream_t stream) {
+    return mgn_adamw_dev2(param, grad, exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, weight_decay, err_word, 1,
+                          stream);
 }
 
 int mgn_abi_version(void) { return MGN_ABI_VERSION; }

@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 11  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 12  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -124,6 +124,7 @@ EXPORTS = {
     "mgn_masked_mse_backward": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _u32, _vp, _vp, _vp, _vp]),
     "mgn_adamw": (_i32, [_vp, _vp, _vp, _vp, _i64, _dbl, _dbl, _dbl, _dbl, _dbl, _i64, _vp]),
     "mgn_adamw_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp, _vp]),
+    "mgn_adamw_dev2": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _dbl, _dbl, _dbl, _dbl, _vp, _i32, _vp]),
     "mgn_coalesce_workspace_bytes": (_sz, [_i64]),
     "mgn_coalesce": (_i32, [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _sz, _vp]),
     "mgn_face_to_edge_keys": (_i64, [_i32, _i64]),

@@ -89,6 +89,10 @@ GRAD_GROUP_BYTES = 4 << 20
 # (mgn_block_backward_deferred2; bit-identical gradients). MGN_PAIR_DE=0: row-major (A/B timing)
 PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
 _SIDE = {}
+# Inspection hook (tests: mask-pinned parity): INSPECT(dict) is called at the end of every training
+# forward of EncodeProcessDecode with the forward saves (topology, plan, per-MLP saved buffers), so a
+# check can read the ReLU branch each hidden unit took. None: no call.
+INSPECT = None
 
 
 def _side_stream(dev):
@@ -526,6 +530,9 @@ class EPDFunction(torch.autograd.Function):
             _mlp_fwd(descs[2], dec, xs[-1], mdt, H, None, N, out, nat.MGN_F32, sv_dec[0], st)
             if dec.out_width != dec.out_dim:  # a decoder whose output width is the (padded) hidden size
                 out = out[:, :dec.out_dim].contiguous()
+        if train and INSPECT is not None:
+            INSPECT(dict(topo=topo, plan=plan, mdt=mdt, only_processor=only_processor, svs=svs, sv_ne=sv_ne,
+                         sv_ee=sv_ee, sv_dec=sv_dec))
         if train:
             ctx.plan, ctx.mdt, ctx.only_processor, ctx.topo = plan, mdt, only_processor, topo
             ctx.pw = pw

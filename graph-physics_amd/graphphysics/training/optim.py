@@ -65,6 +65,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def launch(self):
         """Device side of a step (graph-capturable): the AdamW kernel(s)."""
         L = nat.lib()
+        first = 1  # the skipped-update count of the error word counts steps: only the first launch counts
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps or "flat_state" not in group:
@@ -81,15 +82,18 @@ class FusedAdamW(torch.optim.Optimizer):
             fp, fg = _flat_span(ps), _flat_span([p.grad for p in ps])
             fm, fv = group["flat_state"]
             if fp is not None and fg is not None:
-                nat.check(L.mgn_adamw_dev(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
-                                          nat.ptr(hyper), b1, b2, group["eps"], group["weight_decay"], err, st))
+                nat.check(L.mgn_adamw_dev2(nat.ptr(fp), nat.ptr(fg), nat.ptr(fm), nat.ptr(fv), fp.numel(),
+                                           nat.ptr(hyper), b1, b2, group["eps"], group["weight_decay"], err, first,
+                                           st))
+                first = 0
             else:
                 for p in ps:
                     s = self.state[p]
                     g = p.grad.contiguous()  # held until the launch is enqueued
-                    nat.check(L.mgn_adamw_dev(nat.ptr(p), nat.ptr(g), nat.ptr(s["exp_avg"]),
-                                              nat.ptr(s["exp_avg_sq"]), p.numel(), nat.ptr(hyper), b1, b2,
-                                              group["eps"], group["weight_decay"], err, st))
+                    nat.check(L.mgn_adamw_dev2(nat.ptr(p), nat.ptr(g), nat.ptr(s["exp_avg"]),
+                                               nat.ptr(s["exp_avg_sq"]), p.numel(), nat.ptr(hyper), b1, b2,
+                                               group["eps"], group["weight_decay"], err, first, st))
+                    first = 0
 
     def _init_state(self, group, ps):
         n = sum(p.numel() for p in ps)

@@ -76,6 +76,16 @@ class TrainStep:
         self._static = None  # graph mode: the batch tensors the graph was recorded on
         if self.dp:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
+        # captured data-parallel step: every rank must choose the same between copy-then-replay and a
+        # re-capture (their collective sequences differ), so the choice is agreed on a host-side (gloo)
+        # control group — no device synchronisation, no extra collective on the GPU stream
+        self._ctl = None
+        if self.dp and graph and self.world > 1:
+            if dist.get_backend(group) == "gloo":
+                self._ctl = group if group is not None else dist.group.WORLD
+            else:
+                ranks = dist.get_process_group_ranks(group) if group is not None else None
+                self._ctl = dist.new_group(ranks=ranks, backend="gloo")
 
     @property
     def node_type(self):
@@ -116,9 +126,11 @@ class TrainStep:
                     if st is not None and "step" in st:
                         st["step"] = torch.tensor(float(g["step_count"]))
         sc = self.sched
-        sc.last_epoch -= n
+        sc.last_epoch = max(sc.last_epoch - n, 0)
         if hasattr(sc, "get_lr_factor"):  # CosineWarmupScheduler: closed form
             lrs = [b * sc.get_lr_factor(epoch=sc.last_epoch) for b in sc.base_lrs]
+        elif hasattr(sc, "_get_closed_form_lr"):  # StepLR, CosineAnnealingLR, ExponentialLR, ...
+            lrs = sc._get_closed_form_lr()
         else:
             import warnings
 
@@ -185,6 +197,13 @@ class TrainStep:
         from graphphysics.utils.data import Data
 
         b = self.batch
+        dev = b.x.device
+        # a validation error of an EARLIER step surfaces here with its real skipped-update count
+        try:
+            nat.check_errors(dev)
+        except (IndexError, RuntimeError) as ex:
+            self._raised(ex)
+            raise
         extra = {k: getattr(b, k) for k in ("pos",) if getattr(b, k, None) is not None}
         self.batch = Data(x=b.x.clone(), y=b.y.clone(), edge_attr=b.edge_attr.clone(), edge_index=b.edge_index,
                           **extra)
@@ -192,11 +211,31 @@ class TrainStep:
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            for _ in range(max(warmup, 1)):
-                self.eager()
-        cur.wait_stream(side)
-        torch.cuda.synchronize()
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(max(warmup, 1)):
+                    self.eager()
+            cur.wait_stream(side)
+            torch.cuda.synchronize()
+            nat.check_errors(dev)  # the warm-up steps validated THIS batch
+        except (IndexError, RuntimeError):
+            # the batch is invalid: undo the warm-up steps (their skipped updates and normalizer
+            # accumulations are not the caller's), then run ONE eager step on it — exactly what the
+            # eager path does with a bad batch (the normalizers the reference runs before its raise
+            # accumulate; the device skips the update) — and raise with that step's skip count
+            torch.cuda.synchronize()
+            nat.error_word(dev)._clear()
+            self._restore(snap)
+            self.batch = b
+            self.graph = None
+            self.eager()
+            torch.cuda.synchronize()
+            try:
+                nat.check_errors(dev)
+            except (IndexError, RuntimeError) as ex2:
+                self._raised(ex2)
+                raise
+            raise RuntimeError("libmgn: validation error during graph warm-up did not reproduce eagerly")
         self._restore(snap)
         self.opt.zero_grad(set_to_none=True)
         if on_record is not None:
@@ -281,6 +320,13 @@ class TrainStep:
             raise
         if self.graph is not None:
             self._sync_batch()
+        if self._ctl is not None:
+            # re-capture on every rank if any rank needs to (a rank that copies and
+            # replays while another re-captures would pair mismatched collectives)
+            need = torch.tensor([1 if self.graph is None else 0], dtype=torch.int32)
+            dist.all_reduce(need, op=dist.ReduceOp.MAX, group=self._ctl)
+            if int(need[0]):
+                self.graph = None
         if self.graph is None:
             self.capture()
         self._bind_graph_grads()

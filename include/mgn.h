@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 11
+#define MGN_ABI_VERSION 12
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -367,6 +367,14 @@ int mgn_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq
 int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
                   uint32_t* err_word, mgn_stream_t stream);
+/* ABI v12: as mgn_adamw_dev; a skipped update is counted in err_word's MGN_ERR_SKIP_* field only when
+ * count_skip != 0 — an optimizer step that issues several launches (one per parameter group or
+ * parameter) passes 1 on its first launch and 0 on the others, so the field counts STEPS.
+ * mgn_adamw_dev == mgn_adamw_dev2(..., count_skip = 1, ...). Replaces the same optimizer step as
+ * mgn_adamw (reference lightning_module.py:275-282). */
+int mgn_adamw_dev2(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   const double* hyper, double beta1, double beta2, double eps, double weight_decay,
+                   uint32_t* err_word, int32_t count_skip, mgn_stream_t stream);
 
 /* ---------------------------------------------------------------- graph construction */
 /* On-device replacements for the reference's per-sample host preprocessing (SURVEY.md §8(f)

@@ -33,39 +33,47 @@ def rmsnorm(x, scale, eps=1e-8):
     return scale * (x / (r + eps))
 
 
-def mlp(x, p, prefix, n_linear=4, norm=True):
-    """p: state-dict-like mapping; linears at Sequential indices 0,2,4,...; RMSNorm at 2L-1."""
+def mlp(x, p, prefix, n_linear=4, norm=True, masks=None, record=None):
+    """p: state-dict-like mapping; linears at Sequential indices 0,2,4,...; RMSNorm at 2L-1.
+    masks (test infrastructure, mask-pinned parity): {prefix: [bool [rows, h] per hidden layer]} — the
+    ReLU of hidden layer i becomes h * masks[prefix][i] (the same function on the branch those masks
+    select: identical to relu wherever the mask equals (h > 0)). record: {prefix: [pre-activations]}."""
     h = x
+    pin = masks.get(prefix) if masks is not None else None
     for i in range(n_linear):
         h = F.linear(h, p[f"{prefix}.{2 * i}.weight"], p[f"{prefix}.{2 * i}.bias"])
         if i < n_linear - 1:
-            h = torch.relu(h)
+            if record is not None:
+                record.setdefault(prefix, []).append(h.detach())
+            h = h * pin[i].to(h.dtype) if pin is not None else torch.relu(h)
     if norm:
         h = rmsnorm(h, p[f"{prefix}.{2 * n_linear - 1}.scale"])
     return h
 
 
-def graph_net_block(x, edge_index, e, p, prefix=""):
+def graph_net_block(x, edge_index, e, p, prefix="", masks=None, record=None):
     row, col = edge_index[0], edge_index[1]
-    m = mlp(torch.cat([e, x[col], x[row]], dim=-1), p, prefix + "edge_block")
+    m = mlp(torch.cat([e, x[col], x[row]], dim=-1), p, prefix + "edge_block", masks=masks, record=record)
     aggr = m.new_zeros((x.size(0), m.size(1))).scatter_add_(
         0, col.view(-1, 1).expand_as(m), m)
-    upd = mlp(torch.cat([x, aggr], dim=-1), p, prefix + "node_block")
+    upd = mlp(torch.cat([x, aggr], dim=-1), p, prefix + "node_block", masks=masks, record=record)
     e_new = e + m  # residual order as layers.py:698-699 (edge first: autograd accumulation order)
     return x + upd, e_new
 
 
-def encode_process_decode(graph_x, edge_index, graph_e, p, mp, only_processor=False):
+def encode_process_decode(graph_x, edge_index, graph_e, p, mp, only_processor=False, masks=None, record=None):
+    """masks / record: see mlp (mask-pinned parity checks; default: the reference's ReLUs)."""
+    kw = dict(masks=masks, record=record)
     if only_processor:
         x, e = graph_x, graph_e
     else:
-        x = mlp(graph_x, p, "nodes_encoder")
-        e = mlp(graph_e, p, "edges_encoder")
+        x = mlp(graph_x, p, "nodes_encoder", **kw)
+        e = mlp(graph_e, p, "edges_encoder", **kw)
     for b in range(mp):
-        x, e = graph_net_block(x, edge_index, e, p, f"processor_list.{b}.")
+        x, e = graph_net_block(x, edge_index, e, p, f"processor_list.{b}.", **kw)
     if only_processor:
         return x
-    return mlp(x, p, "decode_module", norm=False)
+    return mlp(x, p, "decode_module", norm=False, **kw)
 
 
 # --------------------------------------------------------------------------- module form

@@ -44,3 +44,33 @@ def test_permutation_changes_the_summation_order():
     ref = {k: v.grad.clone() for k, v in rp.items()}
     sp = order_spread(loss, rp, {k: v.double() for k, v in ref.items()}, n_orders=1)
     assert max(sp.values()) > 0.0
+
+
+def test_mask_pinned_oracle_and_r8_decode():
+    """Mask pinning (tests/_masks.py): the oracle on the natural ReLU branch is bitwise the reference
+    ops; on a branch with one unit flipped it differs only downstream of that unit; the R8 decode
+    inverts the row-octet layout of include/mgn.h mgn_mlp_saved."""
+    from _masks import _r8, flips
+
+    ei, x, ea, gy, rp = _case(mp=2, h=16)
+    rec = {}
+    y0 = O.encode_process_decode(x, ei, ea, rp, 2)
+    y1 = O.encode_process_decode(x, ei, ea, rp, 2, masks=None, record=rec)
+    masks = {k: [z > 0 for z in v] for k, v in rec.items()}
+    y2 = O.encode_process_decode(x, ei, ea, rp, 2, masks=masks)
+    assert torch.equal(y0, y1) and torch.equal(y0, y2)
+    assert flips(masks, rec) == {}
+    m2 = {k: [t.clone() for t in v] for k, v in masks.items()}
+    m2["decode_module"][2][5, 3] ^= True
+    f = flips(m2, rec)
+    assert list(f) == ["decode_module.4"] and f["decode_module.4"]["flipped"] == 1
+    y3 = O.encode_process_decode(x, ei, ea, rp, 2, masks=m2)
+    assert torch.equal((y3 != y0).any(1).nonzero().flatten(), torch.tensor([5]))
+    # R8: element (m, c) at ((m/8)·cols + c)·8 + m%8, rows padded to 64
+    rows, cols = 70, 12
+    a = torch.arange(rows * cols, dtype=torch.float32).view(rows, cols)
+    buf = torch.zeros(128 * cols + 5)
+    for m in range(rows):
+        for c in range(cols):
+            buf[5 + ((m // 8) * cols + c) * 8 + m % 8] = a[m, c]
+    assert torch.equal(_r8(buf, 5, rows, cols), a)

@@ -180,14 +180,16 @@ def test_bad_node_type_step_leaves_state_like_reference(graph, bad):
     assert not all(torch.equal(a, b) for a, b in zip([p.detach() for p in sim.parameters()], before["params"]))
 
 
-def test_bad_edge_index_skips_the_optimizer_update():
+@pytest.mark.parametrize("graph", [False, True])
+def test_bad_edge_index_skips_the_optimizer_update(graph):
     """An out-of-range edge_index (eager path: the topology is rebuilt for the new tensor) raises
     IndexError lazily; the device skipped AdamW for every step since, and the host counters rewind.
-    The normalisers accumulated (the reference's gather raises in the model, after the Simulator
-    preamble)."""
+    The normalisers accumulated once (the reference's gather raises in the model, after the Simulator
+    preamble). Graph mode: the new edge_index forces a re-capture, whose warm-up steps find the error;
+    they are undone and the batch runs once eagerly, so the state is the eager path's."""
     from graphphysics.utils.data import Data
 
-    sim, opt, sch, st = _train(False)
+    sim, opt, sch, st = _train(graph)
     good = st.batch
     st()
     torch.cuda.synchronize()
