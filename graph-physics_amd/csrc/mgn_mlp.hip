@@ -757,10 +757,20 @@ struct WgJob {
     int32_t layer, kb, n, k, kp, staged;  // staged: B operand re-gathered from seg[] through LDS
     int64_t w_off, b_off, act_off;        // b_off < 0: no bias for this job
     int32_t zl, pad;                      // dZ operand = R8 block zl of dz8
+    // multi-MLP launches (WgArgs.multi): the job's own rows, operands, slabs and (staged) segment —
+    // one launch then covers every weight gradient of a GraphNetBlock (edge MLP over edge rows, node
+    // MLP and the edge W0's x blocks over node rows); blockIdx.x >= nchunks: idle workgroup
+    int64_t RP, M;
+    int32_t rows_per_chunk, nchunks;
+    const void* dz8;
+    const void* act8;
+    float* part;
+    int64_t G;
+    SrcSeg seg;
 };
 struct WgArgs {
     int64_t RP, M;
-    int32_t rows_per_chunk, H, njobs, gathered, nseg, pad;
+    int32_t rows_per_chunk, H, njobs, gathered, nseg, multi;
     const void* dz8;
     const void* act8;
     SrcSeg seg[3];  // gathered != 0: layer-0 input segments (re-gathered, staged through LDS)
@@ -795,14 +805,27 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     const int grp = threadIdx.x / MGN_THREADS, tid = threadIdx.x % MGN_THREADS;
     T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * H * LDT;  // this group's [2][H][LDT]
     const WgJob job = a.job[blockIdx.y];
-    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_chunk;
-    const int64_t r_end = r_begin + a.rows_per_chunk < a.RP ? r_begin + a.rows_per_chunk : a.RP;
+    const bool multi = a.multi != 0;
+    if (multi && (int)blockIdx.x >= job.nchunks) return;  // uniform per workgroup, before any barrier
+    const int64_t RP = multi ? job.RP : a.RP, Mrows = multi ? job.M : a.M, G = multi ? job.G : a.G;
+    const int RPC = multi ? job.rows_per_chunk : a.rows_per_chunk;
+    const void* dz8 = multi ? job.dz8 : a.dz8;
+    const void* act8 = multi ? job.act8 : a.act8;
+    float* const part0 = multi ? job.part : a.part;
+    auto pick_seg = [&](int col0_) {
+        if (multi) return job.seg;
+        int s = 0;
+        while (s + 1 < a.nseg && col0_ >= a.seg[s + 1].coff) ++s;
+        return a.seg[s];
+    };
+    const int64_t r_begin = (int64_t)blockIdx.x * RPC;
+    const int64_t r_end = r_begin + RPC < RP ? r_begin + RPC : RP;
     const int lane = tid & 63, wave = tid >> 6;
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
     const bool active = mt0 < NT;
-    const T* Z = reinterpret_cast<const T*>(a.dz8) + (int64_t)job.zl * a.RP * H;
-    const T* X = reinterpret_cast<const T*>(a.act8) + job.act_off;
+    const T* Z = reinterpret_cast<const T*>(dz8) + (int64_t)job.zl * RP * H;
+    const T* X = reinterpret_cast<const T*>(act8) + job.act_off;
     const int col0 = job.kb * H;
     const bool staged = job.staged != 0;
     bool kon[C::MTW];
@@ -932,9 +955,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             // blocks per fragment). Chunk ch of row r sits at slot ch ^ swz(r), which keeps both the
             // row writes and the transposed reads (a 32-lane half = two blocks 8 rows apart, same
             // columns) conflict-free.
-            int s = 0;
-            while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
-            const SrcSeg g = a.seg[s];
+            const SrcSeg g = pick_seg(col0);
             const T* src = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
             constexpr int CPR = H / 8;                        // 16-byte chunks per row
             constexpr int ITEMS = SR * CPR;
@@ -949,7 +970,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                         const int it = tid + q * MGN_THREADS;
                         const int r = (it / CPR) % SR, ch = it % CPR;
                         const int64_t row = m0 + r;
-                        const bool ok = it < ITEMS && m0 < r_end && row < a.M;
+                        const bool ok = it < ITEMS && m0 < r_end && row < Mrows;
                         const int64_t rc = ok ? row : 0;
                         const int64_t sr = g.idx ? (int64_t)g.idx[rc] : rc;
                         nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + ch * 8);
@@ -982,9 +1003,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
         // re-gathered layer-0 input: segment holding columns [col0, col0 + H) (segments are H
         // wide); consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the
         // transposed LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots.
-        int s = 0;
-        while (s + 1 < a.nseg && col0 >= a.seg[s + 1].coff) ++s;
-        const SrcSeg g = a.seg[s];
+        const SrcSeg g = pick_seg(col0);
         const T* src = reinterpret_cast<const T*>(g.p);
         constexpr int ITEMS = SR * (H / CH);
         constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;  // 16-byte chunks per thread
@@ -997,7 +1016,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                     const int r = it % SR, cc = (it / SR) * CH;
                     const int64_t row = m0 + r;
                     nxt[q] = u32x4{0u, 0u, 0u, 0u};
-                    if (it < ITEMS && m0 < r_end && row < a.M) {
+                    if (it < ITEMS && m0 < r_end && row < Mrows) {
                         const int64_t sr = g.idx ? (int64_t)g.idx[row] : row;
                         nxt[q] = *reinterpret_cast<const u32x4*>(src + sr * g.ld + (col0 - g.coff) + cc);
                     }
@@ -1056,9 +1075,9 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     __syncthreads();
     if (grp == 0 && active) deposit(true);
     __syncthreads();
-    float* part = a.part + (int64_t)blockIdx.x * a.G;
+    float* part = part0 + (int64_t)blockIdx.x * G;
     constexpr int C4 = H / 4;
-    const bool vec = ((a.G | job.w_off | (int64_t)job.k) & 3) == 0;
+    const bool vec = ((G | job.w_off | (int64_t)job.k) & 3) == 0;
     for (int it = threadIdx.x; it < H * C4; it += MGN_THREADS * WG_GROUPS) {
         const int n = it / C4, k4 = (it % C4) * 4;
         const int kc = col0 + k4;
@@ -2660,6 +2679,129 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
 
 
 
+// Every weight gradient of a GraphNetBlock on the GENERIC kernels (hidden 16/32/64, fp32 or bf16: the
+// small configurations — training_config/cylinder.json h=32 fp32, plate.json h=64) in ONE
+// mlp_wgrad_kernel launch of per-job operands (WgArgs.multi), jobs and chunking as block_wgrad_ring:
+// the edge MLP over edge rows (e block of W0, layers 1-3), the node MLP over node rows ([x ‖ aggr]
+// blocks of W0, layers 1-3), the edge W0's x blocks over node rows (dP_i / dP_j, into the edge
+// slabs' x-block columns). Replaces 3 weight-gradient launches + 2 reductions per block (the
+// reduction joins the deferred one, mgn_wgrad_reduce_many). Every dZ (layer 0 included) is R8.
+template <class T, int H>
+int block_wgrad_generic(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradIn& in, hipStream_t st,
+                        RedDesc* defer = nullptr) {
+    const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
+    auto rows_for = [](int64_t RP, int64_t target, int* nch) {
+        int64_t c = cdiv64(RP, target);
+        const int64_t cmax = wgrad_max_chunks(RP);
+        if (c > cmax) c = cmax;
+        if (c < 1) c = 1;
+        int64_t r = cdiv64(cdiv64(RP, c), 64) * 64;
+        *nch = (int)cdiv64(RP, r);
+        return (int)r;
+    };
+    const int cus = device_cus();
+    int ce = 1, cn = 1, cp = 1, re = 0, rn = 0, rp = 0;
+    {
+        const int64_t total = 4 * RPE + 7 * RPN;
+        for (int64_t target = cdiv64(cdiv64(total, cus), 64) * 64;; target += 64) {
+            re = rows_for(RPE, target, &ce);
+            rn = rows_for(RPN, target, &cn);
+            if (4 * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
+        }
+        const int64_t cpmax = wgrad_max_chunks(RPE);
+        const int64_t c = cn < cpmax ? cn : cpmax;
+        rp = (int)(cdiv64(cdiv64(RPN, c), 64) * 64);
+        cp = (int)cdiv64(RPN, rp);
+    }
+    WgArgs a;
+    memset(&a, 0, sizeof(a));
+    a.H = H;
+    a.multi = 1;
+    a.gathered = 1;
+    int nj = 0, maxch = 0;
+    const int dt = dtype_id<T>();
+    auto add = [&](int layer, int kb, int n, int k, int kp, const void* dz, const void* act, int64_t act_offv,
+                   const void* seg_p, int64_t RP, int64_t M, float* part, int64_t Gm, int64_t w_off, int64_t b_off,
+                   int rows, int nch) {
+        WgJob& j = a.job[nj++];
+        j.layer = layer;
+        j.kb = kb;
+        j.n = n;
+        j.k = k;
+        j.kp = kp;
+        j.staged = seg_p != nullptr;
+        j.w_off = w_off;
+        j.b_off = b_off;
+        j.act_off = act_offv;
+        j.zl = 0;
+        j.RP = RP;
+        j.M = M;
+        j.rows_per_chunk = rows;
+        j.nchunks = nch;
+        j.dz8 = dz;
+        j.act8 = act;
+        j.part = part;
+        j.G = Gm;
+        j.seg = SrcSeg{seg_p, nullptr, H, H, dt, kb * H, 0};
+        if (nch > maxch) maxch = nch;
+    };
+    const T* edz = reinterpret_cast<const T*>(in.edz8);
+    const T* ndz = reinterpret_cast<const T*>(in.ndz8);
+    const T* dP = reinterpret_cast<const T*>(in.dP8);
+    const int64_t Ge = grad_G(edge), Gn = grad_G(node);
+    int64_t off = 0;
+    for (int l = 0; l < edge->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*edge, l, &n, &k);
+        const T* z = edz + (int64_t)l * RPE * H;
+        if (l == 0)
+            add(0, 0, n, k, k, z, nullptr, 0, in.e, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, re, ce);
+        else
+            add(l, 0, n, k, act_cols(*edge, l), z, in.eact, act_off(*edge, in.E, l, 1), nullptr, RPE, in.E, in.epart,
+                Ge, off, off + (int64_t)n * k, re, ce);
+        off += (int64_t)n * k + n;
+    }
+    off = 0;
+    for (int l = 0; l < node->n_layers; ++l) {
+        int n, k;
+        mlp_layer_shape(*node, l, &n, &k);
+        const T* z = ndz + (int64_t)l * RPN * H;
+        if (l == 0) {
+            add(0, 0, n, k, k, z, nullptr, 0, in.x, RPN, in.N, in.npart, Gn, off, off + (int64_t)n * k, rn, cn);
+            add(0, 1, n, k, k, z, nullptr, 0, in.aggr, RPN, in.N, in.npart, Gn, off, -1, rn, cn);
+        } else {
+            add(l, 0, n, k, act_cols(*node, l), z, in.nact, act_off(*node, in.N, l, 1), nullptr, RPN, in.N, in.npart,
+                Gn, off, off + (int64_t)n * k, rn, cn);
+        }
+        off += (int64_t)n * k + n;
+    }
+    for (int s2 = 0; s2 < 2; ++s2)
+        add(0, 1 + s2, H, edge->in_dim, edge->in_dim, dP + (int64_t)s2 * RPN * H, nullptr, 0, in.x, RPN, in.N,
+            in.epart, Ge, 0, -1, rp, cp);
+    a.njobs = nj;
+    auto fn = mlp_wgrad_kernel<T, H>;
+    size_t lds = wgrad_lds_bytes<T, H>(true);
+    if (wgrad_lds_bytes<T, H>(false) > lds) lds = wgrad_lds_bytes<T, H>(false);
+    if (int e = set_lds((const void*)fn, lds)) return e;
+    {
+        ProfScope ps(PROF_WGRAD, st);
+        hipLaunchKernelGGL(fn, dim3(maxch, nj), dim3(MGN_THREADS * WG_GROUPS), lds, st, a);
+        MGN_LAUNCH_CHECK();
+    }
+    RedDesc d[2] = {red_desc(edge, in.epart, ce, in.edsp, in.entiles, in.egrads),
+                    red_desc(node, in.npart, cn, in.ndsp, in.nntiles, in.ngrads)};
+    d[0].w0_n = H;
+    d[0].w0_k = edge->in_dim;
+    d[0].xcol0 = H;
+    d[0].nchunks_x = cp;
+    if (defer) {
+        defer[0] = d[0];
+        defer[1] = d[1];
+        return 0;
+    }
+    return launch_reduce2(d, 2, st);
+}
+
 size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     const size_t es = m->dtype == MGN_F32 ? 4 : 2;
     // dscale partial rows: the most any backward kernel writes (generic: one per 32-row tile;
@@ -3125,41 +3267,87 @@ int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int32_t block_mlp, int64
     return 0;
 }
 
+// keep != NULL: the dscale partials and weight-gradient slabs go to `keep` (mlp_keep_bytes) and the
+// reduction is left to the caller (*defer); else they are carved from ws and reduced here.
+static size_t mlp_keep_bytes(const mgn_mlp* m, int64_t rows) {
+    const int64_t ntiles = rows_pad(rows) / 16;  // the most any backward kernel writes (as mlp_bwd_ws)
+    return align_up((size_t)ntiles * m->out_dim * sizeof(float)) +
+           align_up((size_t)wgrad_max_chunks(rows_pad(rows)) * grad_G(m) * sizeof(float));
+}
+
+static int mlp_backward_entry(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
+                              int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,
+                              int32_t din_dtype, float* grads, void* ws, size_t ws_bytes, void* keep, RedDesc* defer,
+                              hipStream_t st) {
+    if (int e = check_mlp(m)) return e;
+    MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, rows), "backward workspace too small");
+    const bool chained = chain_dense_eligible(m) && rows > 0;
+    const size_t es = m->dtype == MGN_F32 ? 4 : 2;
+    int ntiles = (int)(rows_pad(rows) / bm_host(m->dtype, MODE_DENSE));
+    char* p = reinterpret_cast<char*>(ws);
+    void* dz = p;
+    p += align_up((size_t)m->n_layers * rows_pad(rows) * m->hidden * (chained ? 2 : es));
+    char* q = keep ? reinterpret_cast<char*>(keep) : p;
+    float* dsp = reinterpret_cast<float*>(q);
+    q += align_up((size_t)(keep ? rows_pad(rows) / 16 : ntiles) * m->out_dim * sizeof(float));
+    float* part = reinterpret_cast<float*>(q);
+    if (rows == 0) {
+        MGN_TRY(hipMemsetAsync(grads, 0, (grad_G(m) + (m->has_norm ? m->out_dim : 0)) * sizeof(float), st));
+        return 0;
+    }
+    if (chained) {
+        // chained data gradients (dZ of every layer, din) + the generic weight gradients over the
+        // same R8 operands
+        MGN_REQUIRE(dout_dtype == MGN_F32 || dout_dtype == MGN_BF16, "dout dtype must be MGN_F32 or MGN_BF16");
+        if (int e = chain16_dense_backward(m, rows, saved, dout, dout_dtype, din, din_dtype, m->in_dim, dz, dsp,
+                                           &ntiles, st))
+            return e;
+    } else {
+        BwdOut o;
+        memset(&o, 0, sizeof(o));
+        o.mode = MODE_DENSE;
+        o.din = din;
+        o.din_dtype = din_dtype;
+        o.din_ld = m->in_dim;
+        if (int e = mlp_bwd_any(m, MODE_DENSE, rows, saved, dout, dout_dtype, m->out_dim, o, dz, dsp, st)) return e;
+    }
+    int nchunks = 0;
+    if (int e = mlp_wgrad_any(m, rows, saved->act, dz, dsp, ntiles, part, grads, nullptr, 0, &nchunks, defer == nullptr,
+                              st))
+        return e;
+    if (defer) *defer = red_desc(m, part, nchunks, dsp, ntiles, grads);
+    return 0;
+}
+
 int mgn_mlp_backward(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
                      int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,
                      int32_t din_dtype, float* grads, void* ws, size_t ws_bytes, mgn_stream_t stream) {
+    (void)in;
+    (void)in_dtype;
+    (void)in_ld;
+    (void)in_rows;  // a dense MLP's layer-0 input is in its R8 saves
+    return mlp_backward_entry(m, in, in_dtype, in_ld, in_rows, rows, saved, dout, dout_dtype, din, din_dtype, grads, ws,
+                              ws_bytes, nullptr, nullptr, (hipStream_t)stream);
+}
+
+size_t mgn_mlp_backward_keep_bytes(const mgn_mlp* m, int64_t rows) { return mlp_keep_bytes(m, rows); }
+
+int mgn_mlp_backward_deferred(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                              const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved, const void* dout,
+                              int32_t dout_dtype, void* din, int32_t din_dtype, float* grads, void* ws,
+                              size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce1,
+                              mgn_stream_t stream) {
+    MGN_REQUIRE(reduce1 && keep, "keep buffer and reduce1 required");
+    memset(reduce1, 0, sizeof(mgn_wgrad_reduce));
     if (int e = check_mlp(m)) return e;
-    if (chain_dense_eligible(m) && rows > 0) {
-        // chained data gradients (dZ of every layer, din) + the generic weight gradients over the
-        // same R8 operands; workspace carve as mlp_backward_impl: dz | dscale partials | slabs
-        MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, rows), "backward workspace too small");
-        MGN_REQUIRE(dout_dtype == MGN_F32 || dout_dtype == MGN_BF16, "dout dtype must be MGN_F32 or MGN_BF16");
-        hipStream_t st = (hipStream_t)stream;
-        const int ntiles = (int)(rows_pad(rows) / bm_host(m->dtype, MODE_DENSE));
-        char* p = reinterpret_cast<char*>(ws);
-        void* dz = p;
-        p += align_up((size_t)m->n_layers * rows_pad(rows) * m->hidden * 2);
-        float* dsp = reinterpret_cast<float*>(p);
-        p += align_up((size_t)ntiles * m->out_dim * sizeof(float));
-        float* part = reinterpret_cast<float*>(p);
-        int nparts = 0;
-        if (int e = chain16_dense_backward(m, rows, saved, dout, dout_dtype, din, din_dtype, m->in_dim, dz, dsp,
-                                           &nparts, st))
-            return e;
-        return mlp_wgrad_any(m, rows, saved->act, dz, dsp, nparts, part, grads, nullptr, 0, nullptr, true, st);
-    }
-    MlpIn mi;
-    memset(&mi, 0, sizeof(mi));
-    mi.seg[0] = SrcSeg{in, in_rows, in_ld, m->in_dim, in_dtype, 0, 0};
-    mi.nseg = 1;
-    BwdOut o;
-    memset(&o, 0, sizeof(o));
-    o.mode = MODE_DENSE;
-    o.din = din;
-    o.din_dtype = din_dtype;
-    o.din_ld = m->in_dim;
-    return mlp_backward_impl(m, MODE_DENSE, rows, mi, saved, dout, dout_dtype, m->out_dim, o, grads, ws, ws_bytes,
-                             (hipStream_t)stream);
+    MGN_REQUIRE(keep_bytes >= mlp_keep_bytes(m, rows), "mlp backward keep buffer too small");
+    RedDesc d;
+    memset(&d, 0, sizeof(d));
+    if (int e = mlp_backward_entry(m, in, in_dtype, in_ld, in_rows, rows, saved, dout, dout_dtype, din, din_dtype, grads,
+                                   ws, ws_bytes, keep, &d, (hipStream_t)stream))
+        return e;
+    memcpy(reduce1, &d, sizeof(d));
+    return 0;
 }
 
 static size_t block_fwd_ws(const mgn_topology* t, const mgn_mlp* edge) {
@@ -3302,6 +3490,7 @@ size_t mgn_block_backward_workspace_bytes(const mgn_topology* t, const mgn_mlp* 
 // on another stream, overlapped with the next block's _data on a second workspace (the hot path:
 // the bandwidth-bound weight-gradient launch fills the CUs the latency-bound node kernels leave idle).
 struct BlockBwdCarve {
+    bool gen1;       // generic MLPs of hidden < 128: one multi-job weight-gradient launch (block_wgrad_generic)
     void *mlp_ws, *dx_part, *d_aggr, *dz0, *dP8;
     void* ndz;       // chained / ring32: node dZ saves (R8)
     float* ndsp;     // chained / ring32: node dscale partials
@@ -3320,6 +3509,15 @@ static bool ring_f32_eligible(const mgn_topology* t, const mgn_mlp* edge, const 
            node->hidden == 128 && edge->n_layers == 4 && node->n_layers == 4 && edge->in_dim == 3 * 128 &&
            node->in_dim == 2 * 128 && edge->out_dim == 128 && node->out_dim == 128 && t->num_nodes > 0 &&
            t->num_edges > 0;
+}
+
+// generic blocks of hidden < 128 (cylinder.json h=32 fp32, plate.json h=64 bf16): the node MLP keeps its
+// dZ saves for ONE multi-job weight-gradient launch per block (block_wgrad_generic)
+static bool gen1_eligible(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    const int H = edge->hidden;
+    return (H == 16 || H == 32 || H == 64) && node->hidden == H && edge->dtype == node->dtype &&
+           edge->n_layers == 4 && node->n_layers == 4 && edge->in_dim == 3 * H && node->in_dim == 2 * H &&
+           edge->out_dim == H && node->out_dim == H && t->num_nodes > 0 && t->num_edges > 0;
 }
 
 // Deferred-reduction "keep" buffer of one block: the RMSNorm-scale partial rows and the weight-
@@ -3357,7 +3555,8 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dP8 = w + wl.dP8;
     c.chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
     c.ring32 = !c.chained && ring_f32_eligible(t, edge, node);
-    if (c.chained || c.ring32) {
+    c.gen1 = !c.chained && !c.ring32 && gen1_eligible(t, edge, node);
+    if (c.chained || c.ring32 || c.gen1) {
         const int64_t Nn = t->num_nodes;
         char* q = w + wl.nmlp;
         c.ndz = q;
@@ -3375,7 +3574,7 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dsp = reinterpret_cast<float*>(p);
     p += align_up((size_t)ntiles * edge->out_dim * sizeof(float));
     c.part = reinterpret_cast<float*>(p);
-    if (keep && (c.chained || c.ring32)) {
+    if (keep && (c.chained || c.ring32 || c.gen1)) {
         const KeepLayout k = keep_layout(t, edge, node);
         char* q = reinterpret_cast<char*>(keep);
         c.dsp = reinterpret_cast<float*>(q + k.edsp);
@@ -3420,8 +3619,9 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         if (int r = chain16_node_backward(node, t->num_nodes, &saved->node, dx_out, c.ndz, c.ndsp, &nparts, c.dx_part,
                                           c.d_aggr, st, flags & MGN_BWD_DX_OUT_PAIR))
             return r;
-    } else if (c.ring32) {
-        // generic fp32 data gradients, dZ saves and dscale partials kept for the block's fp32 ring
+    } else if (c.ring32 || c.gen1) {
+        // generic data gradients, dZ saves and dscale partials kept for the block's single
+        // weight-gradient launch (the fp32 ring, or block_wgrad_generic)
         MGN_REQUIRE(wl.dxpart - wl.nmlp >= mlp_bwd_ws(node, t->num_nodes), "backward workspace too small");
         BwdOut on;
         memset(&on, 0, sizeof(on));
@@ -3518,7 +3718,7 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         in.ngrads = node_grads;
         return block_wgrad_ring<__bf16>(edge, node, in, st, keep ? defer : nullptr);
     }
-    if (c.ring32) {
+    if (c.ring32 || c.gen1) {
         BlockWgradIn in;
         in.E = E;
         in.N = N;
@@ -3530,16 +3730,23 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         in.dz0 = c.dz0;
         in.dP8 = c.dP8;
         in.edsp = c.dsp;
-        in.entiles = (int)(rows_pad(E) / bm_host(MGN_F32, MODE_EDGE));
+        in.entiles = (int)(rows_pad(E) / bm_host(dt, MODE_EDGE));
         in.epart = c.part;
         in.egrads = edge_grads;
         in.nact = saved->node.act;
         in.ndz8 = c.ndz;
         in.ndsp = c.ndsp;
-        in.nntiles = (int)(rows_pad(N) / bm_host(MGN_F32, MODE_NODE));
+        in.nntiles = (int)(rows_pad(N) / bm_host(dt, MODE_NODE));
         in.npart = c.npart;
         in.ngrads = node_grads;
-        return block_wgrad_ring<float>(edge, node, in, st, keep ? defer : nullptr);
+        if (c.ring32) return block_wgrad_ring<float>(edge, node, in, st, keep ? defer : nullptr);
+        int rc = 0;
+        if (dt == MGN_F32) {
+            MGN_DISPATCH_H(H, rc = (block_wgrad_generic<float, HH>(edge, node, in, st, keep ? defer : nullptr)))
+        } else {
+            MGN_DISPATCH_H(H, rc = (block_wgrad_generic<__bf16, HH>(edge, node, in, st, keep ? defer : nullptr)))
+        }
+        return rc;
     }
     // weight gradients: edge rows (e block of W0 + layers 1..), node rows (x blocks of W0), one reduce
     const int ntiles = chain_eligible(edge) ? chain16_edge_backward_parts(E) : (int)(rows_pad(E) / bm_host(dt, MODE_EDGE));
@@ -3598,7 +3805,7 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     const bool chained = (chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0) ||
-                         ring_f32_eligible(t, edge, node);
+                         ring_f32_eligible(t, edge, node) || gen1_eligible(t, edge, node);
     if (!chained) {  // generic MLPs: reduced at once, nothing left for the caller
         MGN_REQUIRE(!flags, "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
         if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,

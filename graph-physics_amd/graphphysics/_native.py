@@ -78,6 +78,10 @@ EXPORTS = {
     "mgn_mlp_saved_elems": (_i32, [ctypes.POINTER(Mlp), _i64, _i32, _vp, _vp]),
     "mgn_mlp_backward": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
                                 ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp]),
+    "mgn_mlp_backward_keep_bytes": (_sz, [ctypes.POINTER(Mlp), _i64]),
+    "mgn_mlp_backward_deferred": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
+                                         ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp, _sz,
+                                         ctypes.POINTER(WgradReduce), _vp]),
     "mgn_block_forward_inference_supported": (_i32, [ctypes.POINTER(Mlp), ctypes.POINTER(Mlp)]),
     "mgn_block_forward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
                                                 ctypes.POINTER(Mlp)]),

@@ -429,6 +429,20 @@ def _mlp_bwd(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, di
         ws.numel() if ws is not None else 0, stream))
 
 
+def _mlp_bwd_deferred(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws,
+                      keep, red, stream):
+    """_mlp_bwd with the reduction left to one mgn_wgrad_reduce_many at the end of the backward."""
+    nat.check(nat.lib().mgn_mlp_backward_deferred(
+        ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld, nat.ptr(rows_idx), rows, ctypes.byref(saved),
+        nat.ptr(dout), dout_mdt, nat.ptr(din), din_mdt, nat.ptr(grads), nat.ptr(ws), ws.numel(), nat.ptr(keep),
+        keep.numel(), red, stream))
+
+
+def _mlp_keep(desc, rows, dev):
+    n = int(nat.lib().mgn_mlp_backward_keep_bytes(ctypes.byref(desc), rows))
+    return torch.empty(max(n, 256), dtype=torch.uint8, device=dev)
+
+
 def _ws_bytes_mlp(desc, rows):
     return int(nat.lib().mgn_mlp_backward_workspace_bytes(ctypes.byref(desc), rows))
 
@@ -565,13 +579,23 @@ class EPDFunction(torch.autograd.Function):
             need = max(need, _ws_bytes_mlp(descs[0], N), _ws_bytes_mlp(descs[1], E),
                        _ws_bytes_mlp(descs[2], N))
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        # encoders' and decoder's reductions deferred into the final mgn_wgrad_reduce_many too (one
+        # reduction launch per backward); not with a gradient-ready callback (its ranges hand over early)
+        defer_dense = DEFER_REDUCE and not ctx.only_processor and GRAD_READY is None and not OVERLAP_WGRAD
+        if defer_dense:
+            dreds = (nat.WgradReduce * 3)()  # decoder, node encoder, edge encoder
+            keeps = [_mlp_keep(descs[2], N, dev), _mlp_keep(descs[0], N, dev), _mlp_keep(descs[1], E, dev)]
         if ctx.only_processor:
             dx = _padc(gout.detach(), H).to(tdt).contiguous()
         else:
             dx = torch.empty((N, H), dtype=tdt, device=dev)
             g = _padc(gout.detach().float(), plan.specs[2].out_width).contiguous()
-            _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
-                     ctypes.c_void_p(gp + 4 * off[2]), ws, st)
+            if defer_dense:
+                _mlp_bwd_deferred(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
+                                  ctypes.c_void_p(gp + 4 * off[2]), ws, keeps[0], ctypes.pointer(dreds[0]), st)
+            else:
+                _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
+                         ctypes.c_void_p(gp + 4 * off[2]), ws, st)
             ready(G, off[2], off[2] + plan.specs[2].numel)
         nb = len(bdescs) // 2
         # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
@@ -655,7 +679,7 @@ class EPDFunction(torch.autograd.Function):
                 ev.record(side)
                 done[b % 2] = ev
             dx, de = dx1, de1
-        if defer and GRAD_READY is None:
+        if defer and GRAD_READY is None and not defer_dense:
             nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
         if overlap:
             for ev in done:
@@ -672,11 +696,25 @@ class EPDFunction(torch.autograd.Function):
         else:
             ne, ee = plan.specs[0], plan.specs[1]
             gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
-            _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
-                     ctypes.c_void_p(gp + 4 * off[0]), ws, st)
             gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
-            _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
-                     nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
+            if defer_dense:
+                _mlp_bwd_deferred(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
+                                  ctypes.c_void_p(gp + 4 * off[0]), ws, keeps[1], ctypes.pointer(dreds[1]), st)
+                _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                                  nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
+                                  ctypes.pointer(dreds[2]), st)
+                # ONE reduction for the whole model: decoder, every processor block, encoders
+                allr = (nat.WgradReduce * (3 + (2 * nb if defer else 0)))()
+                allr[0] = dreds[0]
+                for i in range(2 * nb if defer else 0):
+                    allr[1 + i] = reds[i]
+                allr[len(allr) - 2], allr[len(allr) - 1] = dreds[1], dreds[2]
+                nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
+            else:
+                _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
+                         ctypes.c_void_p(gp + 4 * off[0]), ws, st)
+                _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                         nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
             gx = gxc
             if nea:
                 gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)

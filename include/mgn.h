@@ -221,7 +221,9 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
  * RMSNorm-scale partials go to `keep` (mgn_block_backward_keep_bytes, one buffer per block, alive
  * until the reduction) and reduce2[0..1] describe the reduction; mgn_wgrad_reduce_many then runs
  * every block's in ONE launch — the same sums in the same order, one launch instead of one per
- * block. Generic MLPs are reduced at once (reduce2 zeroed: nothing to do). */
+ * block. Deferred for the chained bf16 h=128 MLPs, the fp32 h=128 ones (fp32 ring) and (ABI v12) the
+ * generic hidden 16/32/64 MLPs (one multi-job weight-gradient launch per block); other shapes are
+ * reduced at once (reduce2 zeroed: nothing to do). */
 typedef struct mgn_wgrad_reduce {
     const float* part;
     const float* dsp;
@@ -257,6 +259,17 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
                                  void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                  int32_t flags, mgn_stream_t stream);
 int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream);
+/* ABI v12: mgn_mlp_backward (the encoders / decoder of processors.py:71-109, 129-137) with the
+ * reduction deferred like mgn_block_backward_deferred: the RMSNorm-scale partials and weight-gradient
+ * slabs go to `keep` (mgn_mlp_backward_keep_bytes, alive until the reduction) and *reduce1 describes
+ * the reduction for mgn_wgrad_reduce_many — so a whole EncodeProcessDecode backward ends in ONE
+ * reduction launch. */
+size_t mgn_mlp_backward_keep_bytes(const mgn_mlp* m, int64_t rows);
+int mgn_mlp_backward_deferred(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                              const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved,
+                              const void* dout, int32_t dout_dtype, void* din, int32_t din_dtype,
+                              float* grads, void* ws, size_t ws_bytes, void* keep, size_t keep_bytes,
+                              mgn_wgrad_reduce* reduce1, mgn_stream_t stream);
 /* The same backward as two calls over one workspace (same arguments): _data writes dx, de (and, for
  * MLPs outside the chained bf16 h=128 kernels, the node-MLP weight gradients); _wgrad then writes the
  * weight gradients from what _data left in `ws` plus the forward saves, and may run on another
