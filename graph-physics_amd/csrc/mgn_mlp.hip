@@ -449,7 +449,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
                 for (int j = 0; j < Gemm<T, NTH, MT>::C::MTW; ++j) {
                     const int m = g.m_of(j);
                     f4 pp = {0.f, 0.f, 0.f, 0.f};
-                    if (MODE == MODE_EDGE && l == 0 && row0 + m < a.M) {
+                    if (MODE == MODE_EDGE && l == 0 && a.proj && row0 + m < a.M) {
                         // [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]
                         const f4 pi = *reinterpret_cast<const f4*>(a.proj + (int64_t)a.proj_i[row0 + m] * (2 * H) + n);
                         const f4 pj = *reinterpret_cast<const f4*>(a.proj + (int64_t)a.proj_j[row0 + m] * (2 * H) + H + n);
@@ -2283,20 +2283,26 @@ int64_t grad_G(const mgn_mlp* m) {
 // rows per chunk: enough workgroups to fill the chip (~512), at most 64 partial slabs
 // one 512-thread workgroup per CU fits (VGPRs + LDS), so chunks x jobs stays within one wave of
 // workgroups over the CUs (a second, partial round doubles a short launch)
-int wgrad_rows_per_chunk(int64_t RP, int njobs) {
-    int64_t chunks = device_cus() / njobs;
-    if (chunks > 64) chunks = 64;
+// Small hidden sizes (H <= 32: cylinder.json's h = 32): a chunk's slab is tiny (H x 3H floats) and
+// one workgroup per CU leaves the kernel latency-bound (its fp32 path loads fragments straight from
+// global memory), so those launches cut the rows into up to 4 x CUs chunks (several workgroups per
+// CU) and up to 256 slabs per job.
+int64_t wgrad_max_chunks(int64_t RP, int H = 128) {
+    const int64_t cap = H <= 32 ? 256 : 64;
+    int64_t c = RP / 64;
+    if (c > cap) c = cap;
+    return c < 1 ? 1 : c;
+}
+int wgrad_wgs_per_cu(int H) { return H <= 32 ? 4 : 1; }
+int wgrad_rows_per_chunk(int64_t RP, int njobs, int H = 128) {
+    int64_t chunks = (int64_t)wgrad_wgs_per_cu(H) * device_cus() / njobs;
+    const int64_t cap = wgrad_max_chunks(RP, H);
+    if (chunks > cap) chunks = cap;
     if (chunks < 1) chunks = 1;
     int64_t r = cdiv64(RP, chunks);
     r = cdiv64(r, 64) * 64;
     if (r < 64) r = 64;
     return (int)r;
-}
-// upper bound of the slab count over any job count (RP is a multiple of 64)
-int64_t wgrad_max_chunks(int64_t RP) {
-    int64_t c = RP / 64;
-    if (c > 64) c = 64;
-    return c < 1 ? 1 : c;
 }
 
 RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* dscale_part, int ntiles,
@@ -2497,7 +2503,7 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8,
         }
         off += (int64_t)n * k + n;
     }
-    a.rows_per_chunk = wgrad_rows_per_chunk(a.RP, nj);
+    a.rows_per_chunk = wgrad_rows_per_chunk(a.RP, nj, H);
     const int nchunks = (int)cdiv64(a.RP, a.rows_per_chunk);
     if (nchunks_out) *nchunks_out = nchunks;
     if (int e = launch_wgrad_kernel<T, H>(a, nj, nchunks, st)) return e;
@@ -2692,14 +2698,14 @@ int block_wgrad_generic(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgr
     const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
     auto rows_for = [](int64_t RP, int64_t target, int* nch) {
         int64_t c = cdiv64(RP, target);
-        const int64_t cmax = wgrad_max_chunks(RP);
+        const int64_t cmax = wgrad_max_chunks(RP, H);
         if (c > cmax) c = cmax;
         if (c < 1) c = 1;
         int64_t r = cdiv64(cdiv64(RP, c), 64) * 64;
         *nch = (int)cdiv64(RP, r);
         return (int)r;
     };
-    const int cus = device_cus();
+    const int cus = wgrad_wgs_per_cu(H) * device_cus();
     int ce = 1, cn = 1, cp = 1, re = 0, rn = 0, rp = 0;
     {
         const int64_t total = 4 * RPE + 7 * RPN;
@@ -2708,7 +2714,7 @@ int block_wgrad_generic(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgr
             rn = rows_for(RPN, target, &cn);
             if (4 * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
         }
-        const int64_t cpmax = wgrad_max_chunks(RPE);
+        const int64_t cpmax = wgrad_max_chunks(RPE, H);
         const int64_t c = cn < cpmax ? cn : cpmax;
         rp = (int)(cdiv64(cdiv64(RPN, c), 64) * 64);
         cp = (int)cdiv64(RPN, rp);
@@ -2807,7 +2813,7 @@ size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     // dscale partial rows: the most any backward kernel writes (generic: one per 32-row tile;
     // chained node kernel: one per workgroup, at most one per 16-row tile)
     const int64_t ntiles = rows_pad(M) / 16;
-    const int64_t nchunks = wgrad_max_chunks(rows_pad(M));
+    const int64_t nchunks = wgrad_max_chunks(rows_pad(M), m->hidden);
     size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
     b += align_up((size_t)nchunks * grad_G(m) * sizeof(float));              // wgrad partial slabs
@@ -3272,7 +3278,7 @@ int mgn_mlp_saved_elems(const mgn_mlp* m, int64_t rows, int32_t block_mlp, int64
 static size_t mlp_keep_bytes(const mgn_mlp* m, int64_t rows) {
     const int64_t ntiles = rows_pad(rows) / 16;  // the most any backward kernel writes (as mlp_bwd_ws)
     return align_up((size_t)ntiles * m->out_dim * sizeof(float)) +
-           align_up((size_t)wgrad_max_chunks(rows_pad(rows)) * grad_G(m) * sizeof(float));
+           align_up((size_t)wgrad_max_chunks(rows_pad(rows), m->hidden) * grad_G(m) * sizeof(float));
 }
 
 static int mlp_backward_entry(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
@@ -3389,8 +3395,12 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     const bool chain = chain_eligible(edge);
     const float* b0 = chain ? edge->bias[0] : nullptr;  // the chained kernel takes b0 from P_i
     MGN_REQUIRE(!proj_ready || chain, "proj_ready: the workspace holds bf16 projections of the chained path only");
+    // Small graphs on the generic kernels (hidden <= 64): layer 0 as the reference's single K = 3h
+    // product over the gathered [e ‖ x_i ‖ x_j] rows (layers.py:689-690) — the node-projection launch
+    // would cost more than the 4h² FLOPs per edge it saves (cylinder.json / plate.json sizes)
+    const bool unsplit = !chain && H <= 64 && t->num_edges > 0 && t->num_edges <= (1 << 18);
     int rc = 0;
-    if (proj_ready) {
+    if (proj_ready || unsplit) {
         // P already in ws: the previous block's node-MLP forward wrote it from its x_out
     } else if (dt == MGN_F32) {
         MGN_DISPATCH_H(H, rc = (launch_proj<float, HH>(edge, x, t->num_nodes, proj, b0, st)))
@@ -3408,6 +3418,13 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     ein.proj = proj;
     ein.proj_i = t->csc_dst;
     ein.proj_j = t->csc_src;
+    if (unsplit) {
+        ein.seg[1] = SrcSeg{x, t->csc_dst, H, H, dt, H, 0};      // x_i = x[edge_index[1]]
+        ein.seg[2] = SrcSeg{x, t->csc_src, H, H, dt, 2 * H, 0};  // x_j = x[edge_index[0]]
+        ein.nseg = 3;
+        ein.K0 = 3 * H;
+        ein.proj = nullptr;
+    }
     if (chain) {
         if (int r = chain16_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st,
                                          chain_node_eligible(node)))
@@ -3533,11 +3550,11 @@ static KeepLayout keep_layout(const mgn_topology* t, const mgn_mlp* edge, const 
     k.edsp = o;
     o += align_up((size_t)(RPE / 16) * edge->out_dim * sizeof(float));
     k.epart = o;
-    o += align_up((size_t)wgrad_max_chunks(RPE) * grad_G(edge) * sizeof(float));
+    o += align_up((size_t)wgrad_max_chunks(RPE, edge->hidden) * grad_G(edge) * sizeof(float));
     k.ndsp = o;
     o += align_up((size_t)(RPN / 16) * node->out_dim * sizeof(float));
     k.npart = o;
-    o += align_up((size_t)wgrad_max_chunks(RPN) * grad_G(node) * sizeof(float));
+    o += align_up((size_t)wgrad_max_chunks(RPN, node->hidden) * grad_G(node) * sizeof(float));
     k.total = o;
     return k;
 }

@@ -120,6 +120,12 @@ def get_topology(edge_index, num_nodes):
     return topo
 
 
+def forget_topology(edge_index):
+    """Drop the cached topology of this edge_index tensor (its next use rebuilds it, re-validating it
+    on the device error word)."""
+    _TOPO_CACHE[:] = [ent for ent in _TOPO_CACHE if ent[0]() is not edge_index]
+
+
 # --------------------------------------------------------------------------- MLPs and plans
 KERNEL_WIDTHS = (16, 32, 64, 128)
 

@@ -223,11 +223,14 @@ class TrainStep:
             # accumulations are not the caller's), then run ONE eager step on it — exactly what the
             # eager path does with a bad batch (the normalizers the reference runs before its raise
             # accumulate; the device skips the update) — and raise with that step's skip count
+            from graphphysics.models import _engine
+
             torch.cuda.synchronize()
             nat.error_word(dev)._clear()
             self._restore(snap)
             self.batch = b
             self.graph = None
+            _engine.forget_topology(b.edge_index)  # its cached (clamped) topology would not re-flag it
             self.eager()
             torch.cuda.synchronize()
             try:

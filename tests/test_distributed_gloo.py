@@ -185,3 +185,81 @@ def test_flat_grad_buffer_detection():
     assert f is not None and f.numel() == 10 and f.data_ptr() == flat.data_ptr()
     b.grad = torch.zeros(6)
     assert flat_grad_buffer([a, b]) is None
+
+
+def _uneven_batch():
+    """7 CylinderFlow graphs; graph g has a g-dependent share of its NORMAL nodes retyped to 6 (not in
+    the loss mask), so every rank's masked-node count differs."""
+    from graphphysics.utils import meshes
+
+    b = meshes.cylinder_batch(7, jitter=0.01)
+    n = b["nodes_per_graph"]
+    x = b["x"].copy()
+    rng = np.random.default_rng(5)
+    for g in range(7):
+        sl = slice(g * n, (g + 1) * n)
+        t = x[sl, 2]
+        t[(t == 0) & (rng.random(n) < 0.06 * g)] = 6
+        x[sl, 2] = t
+    b["x"] = x
+    return b
+
+
+def _shard_graphs(b, lo_g, hi_g):
+    n = b["nodes_per_graph"]
+    lo, hi = lo_g * n, hi_g * n
+    ei = b["edge_index"]
+    keep = (ei[0] >= lo) & (ei[0] < hi)
+    return {"x": b["x"][lo:hi], "y": b["y"][lo:hi], "edge_index": ei[:, keep] - lo, "edge_attr": b["edge_attr"][keep]}
+
+
+SPLIT4 = [(0, 2), (2, 4), (4, 6), (6, 7)]  # 2, 2, 2 graphs and a short last rank with 1
+
+
+def _worker4(rank, world, port, out, prologue):
+    import sys
+
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "graph-physics_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from graphphysics.models.simulator import Simulator
+
+    torch.set_num_threads(1)
+    b = _uneven_batch()
+    d = _shard_graphs(b, *SPLIT4[rank])
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    sim.set_process_group(dist.group.WORLD)
+    loss = _step(sim, d, dist.group.WORLD, prologue)
+    local = int(np.isin(d["x"][:, 2], (0, 5)).sum())
+    dist.all_reduce(loss.detach())
+    res = {"loss": loss.item(), "acc": sim._node_normalizer._acc_sum.clone(),
+           "out_cnt": sim._output_normalizer._acc_count.item(), "local_mask": local,
+           "grads": [p.grad.clone() for p in sim.parameters()]}
+    torch.save(res, os.path.join(out, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("prologue", [False, True])
+def test_four_rank_uneven_shards_equal_single_process_step(prologue):
+    """4 gloo ranks, uneven shards (2/2/2/1 graphs: the last rank short) with a different masked-node
+    count on every rank: the SUM of the per-rank global-mean losses, the all-reduced normaliser
+    statistics and the SUM-all-reduced gradients equal the single-process step on the union
+    (reference loss.py:28-65 masked mean over the whole batch; lightning_module.py:111-122)."""
+    from graphphysics.models.simulator import Simulator
+
+    port = 28500 + os.getpid() % 1000 + 7 * int(prologue)
+    with tempfile.TemporaryDirectory() as out:
+        mp.start_processes(_worker4, args=(4, port, out, prologue), nprocs=4, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(4)]
+    assert len({x["local_mask"] for x in r}) == 4, [x["local_mask"] for x in r]  # really uneven
+    b = _uneven_batch()
+    sim = Simulator(11, 3, 2, 0, 2, 0, 2, 2, _OracleModel(), "cpu")
+    loss = _step(sim, _shard_graphs(b, 0, 7), None)
+    assert abs(r[0]["loss"] - loss.item()) <= 1e-6 * abs(loss.item())
+    assert all(x["out_cnt"] == b["x"].shape[0] for x in r)
+    torch.testing.assert_close(r[3]["acc"], sim._node_normalizer._acc_sum, rtol=1e-5, atol=1e-5)
+    for gs in zip(*(x["grads"] for x in r), sim.parameters()):
+        for g in gs[1:4]:
+            assert torch.equal(gs[0], g)
+        torch.testing.assert_close(gs[0], gs[4].grad, rtol=2e-4, atol=1e-6)
