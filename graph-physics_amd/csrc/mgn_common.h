@@ -186,7 +186,21 @@ __host__ __device__ __forceinline__ int64_t r8_index(int64_t m, int64_t c, int64
 // CUs the persistent kernels size their grids for. MGN_MAX_CUS (read once) caps it, so two streams
 // can each run a persistent kernel on part of the chip at the same time (intra-GPU data parallelism
 // experiments: tools/exp_dual.py).
+// Runtime caps (mgn_set_grid_cus, ABI v13; 0 = none): the persistent grids of every launch except
+// the weight-gradient launches (g_cap_data), and of the weight-gradient launches (g_cap_wgrad), so a
+// block's weight gradients can run on a stream of their own beside the next block's data gradients,
+// each on its own share of the CUs. Read when a launch is issued (a captured graph keeps its grids).
+extern int g_cap_data, g_cap_wgrad;
+inline int hw_cus();
 inline int device_cus() {
+    const int c = hw_cus();
+    return g_cap_data > 0 && g_cap_data < c ? g_cap_data : c;
+}
+inline int wgrad_cus() {
+    const int c = hw_cus();
+    return g_cap_wgrad > 0 && g_cap_wgrad < c ? g_cap_wgrad : c;
+}
+inline int hw_cus() {
     static int cus = 0;
     if (cus == 0) {
         int dev = 0, n = 0;

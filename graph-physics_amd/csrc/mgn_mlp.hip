@@ -2295,7 +2295,7 @@ int64_t wgrad_max_chunks(int64_t RP, int H = 128) {
 }
 int wgrad_wgs_per_cu(int H) { return H <= 32 ? 4 : 1; }
 int wgrad_rows_per_chunk(int64_t RP, int njobs, int H = 128) {
-    int64_t chunks = (int64_t)wgrad_wgs_per_cu(H) * device_cus() / njobs;
+    int64_t chunks = (int64_t)wgrad_wgs_per_cu(H) * wgrad_cus() / njobs;
     const int64_t cap = wgrad_max_chunks(RP, H);
     if (chunks > cap) chunks = cap;
     if (chunks < 1) chunks = 1;
@@ -2588,7 +2588,7 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     // columns (RedDesc x-columns), so the projections need not be cut into ce short chunks. The
     // edge slab buffer holds wgrad_max_chunks(RPE) slabs (keep_layout, mlp_bwd_ws): cp is capped
     // there (graphs with more nodes than edges).
-    const int cus = device_cus();
+    const int cus = wgrad_cus();
     int ce = 1, cn = 1, cp = 1;
     int re = 0, rn = 0, rp = 0;
     {
@@ -2705,7 +2705,7 @@ int block_wgrad_generic(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgr
         *nch = (int)cdiv64(RP, r);
         return (int)r;
     };
-    const int cus = wgrad_wgs_per_cu(H) * device_cus();
+    const int cus = wgrad_wgs_per_cu(H) * wgrad_cus();
     int ce = 1, cn = 1, cp = 1, re = 0, rn = 0, rp = 0;
     {
         const int64_t total = 4 * RPE + 7 * RPN;
@@ -3623,6 +3623,7 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
     hipStream_t st = (hipStream_t)stream;
     const int H = edge->hidden, dt = edge->dtype;
     const BlockBwdCarve c = block_bwd_carve(t, edge, node, ws, wl, keep);
+    flags &= ~(MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY);
     MGN_REQUIRE(!(flags & ~(MGN_BWD_DE_OUT_PAIR | MGN_BWD_DE_PAIR | MGN_BWD_DX_OUT_PAIR | MGN_BWD_DX_PAIR)),
                 "unknown backward layout flags");
     MGN_REQUIRE(!flags || (chain_eligible(edge) && chain_node_eligible(node)),
@@ -3818,11 +3819,18 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
                                  size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                  int32_t flags, mgn_stream_t stream) {
     MGN_REQUIRE(reduce2, "reduce2 (two mgn_wgrad_reduce) required");
-    memset(reduce2, 0, 2 * sizeof(mgn_wgrad_reduce));
+    if (!(flags & MGN_BWD_WGRAD_ONLY)) memset(reduce2, 0, 2 * sizeof(mgn_wgrad_reduce));
     BlockWs wl;
     if (int r = block_bwd_check(t, edge, node, de_out, ws_bytes, &wl)) return r;
     const bool chained = (chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0) ||
                          ring_f32_eligible(t, edge, node) || gen1_eligible(t, edge, node);
+    // a block whose weight gradients cannot be deferred (or keep = NULL) runs whole in its DATA_ONLY
+    // call (reduced at once) and its WGRAD_ONLY call does nothing
+    const int32_t part = flags & (MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY);
+    MGN_REQUIRE(part != (MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY),
+                "MGN_BWD_DATA_ONLY and MGN_BWD_WGRAD_ONLY exclude each other");
+    if ((!chained || !keep) && part == MGN_BWD_WGRAD_ONLY) return 0;
+    flags &= ~(MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY);
     if (!chained) {  // generic MLPs: reduced at once, nothing left for the caller
         MGN_REQUIRE(!flags, "pair-layout de (MGN_BWD_DE_*_PAIR) needs the chained bf16 h=128 edge and node MLPs");
         if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws,
@@ -3839,9 +3847,12 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
                                          nullptr, nullptr, stream);
     }
     MGN_REQUIRE(keep_bytes >= keep_layout(t, edge, node).total, "block backward keep buffer too small");
-    if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
-                                         keep, stream, flags))
-        return r;
+    if (part != MGN_BWD_WGRAD_ONLY) {
+        if (int r = block_backward_data_impl(t, edge, node, x, saved, dx_out, de_out, dx, de, node_grads, ws, ws_bytes,
+                                             keep, stream, flags))
+            return r;
+        if (part == MGN_BWD_DATA_ONLY) return 0;
+    }
     RedDesc d[2];
     memset(d, 0, sizeof(d));
     if (int r = block_backward_wgrad_impl(t, edge, node, x, e, saved, de_out, edge_grads, node_grads, ws, ws_bytes,

@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 12  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 13  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -18,6 +18,8 @@ MGN_BWD_DE_OUT_PAIR = 1  # mgn.h: de_out in the pair layout
 MGN_BWD_DE_PAIR = 2      # mgn.h: write de in the pair layout
 MGN_BWD_DX_OUT_PAIR = 4  # mgn.h: dx_out in the pair layout
 MGN_BWD_DX_PAIR = 8      # mgn.h: write dx in the pair layout
+MGN_BWD_DATA_ONLY = 16   # mgn.h (v13): the data-gradient half of mgn_block_backward_deferred2
+MGN_BWD_WGRAD_ONLY = 32  # mgn.h (v13): its weight-gradient half
 MGN_MAX_LAYERS = 8
 
 _vp = ctypes.c_void_p
@@ -109,6 +111,7 @@ EXPORTS = {
                                             _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
                                             _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_wgrad_reduce_many": (_i32, [ctypes.POINTER(WgradReduce), _i32, _vp]),
+    "mgn_set_grid_cus": (_i32, [_i32, _i32]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),

@@ -88,6 +88,28 @@ GRAD_GROUP_BYTES = 4 << 20
 # deferred path: de / dx handed between consecutive blocks in the pair layout
 # (mgn_block_backward_deferred2; bit-identical gradients). MGN_PAIR_DE=0: row-major (A/B timing)
 PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
+# Processor backward with each block's weight-gradient launch on a side stream, beside the next
+# block's data-gradient kernels (mgn_block_backward_deferred2 MGN_BWD_DATA_ONLY / _WGRAD_ONLY, two
+# workspaces), each on its own share of the CUs (mgn_set_grid_cus). MGN_CONC_WGRAD: "auto" (default:
+# conc_caps below), "0" (one stream), or "data_cus,wgrad_cus" (0,0: both streams uncapped).
+CONC_WGRAD = os.environ.get("MGN_CONC_WGRAD", "auto")
+
+
+def conc_caps(E, chained):
+    """(data CUs, weight-gradient CUs) of the concurrent backward, or None (one stream). "auto": only
+    the chained bf16 h=128 blocks in the latency-bound regime — their persistent edge kernels run 1-4
+    16-row tiles per wave on the whole chip (Cfg B: 1.8) — with the chip split 160 + 96 (measured,
+    Cfg B bf16: 332 -> 342 steps/s; 192 + 64: 297, 128 + 128: 322, both uncapped: 317). Measured
+    slower, so one stream: fp32 Cfg B (its MFMA-bound ring: 98 -> 87), Cfg C at plate.json's sizes
+    (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5 -> 32.7); Cfg A neutral."""
+    v = CONC_WGRAD
+    if v == "0":
+        return None
+    if v != "auto":
+        d, r = (int(t) for t in v.split(","))
+        return d, r
+    tiles_per_wave = E / (16 * 12 * 256)
+    return (160, 96) if chained and 1.0 <= tiles_per_wave <= 4.0 else None
 _SIDE = {}
 # Inspection hook (tests: mask-pinned parity): INSPECT(dict) is called at the end of every training
 # forward of EncodeProcessDecode with the forward saves (topology, plan, per-MLP saved buffers), so a
@@ -636,6 +658,18 @@ class EPDFunction(torch.autograd.Function):
             side = _side_stream(dev)
             wss = [ws, torch.empty_like(ws)]
             done = [None, None]
+        # weight-gradient launches beside the next block's data gradients (the encoders' backward
+        # reuses ws only after the side stream is done with block 1's workspace)
+        caps = conc_caps(E, nb > 0 and all(
+            L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
+            for b in range(nb)))
+        conc = caps is not None and defer and GRAD_READY is None and nb > 1
+        if conc:
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            wss = [torch.empty_like(ws), torch.empty_like(ws)]
+            done = [None, None]
+            nat.check(L.mgn_set_grid_cus(*caps))
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
             de1 = torch.empty((E, H), dtype=tdt, device=dev)
@@ -651,7 +685,22 @@ class EPDFunction(torch.autograd.Function):
                     flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
                 if b > 0:
                     flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
-            if defer:
+            if conc:
+                w = wss[b % 2]
+                if done[b % 2] is not None:
+                    main.wait_event(done[b % 2])  # the side stream is done reading this workspace
+                kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
+                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
+                                                         flags | nat.MGN_BWD_DATA_ONLY, st))
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
+                                                         flags | nat.MGN_BWD_WGRAD_ONLY, nat._vp(side.cuda_stream)))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                done[b % 2] = ev
+            elif defer:
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
                                                          ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
                                                          ctypes.pointer(reds[2 * b]), flags, st))
@@ -685,7 +734,15 @@ class EPDFunction(torch.autograd.Function):
                 ev.record(side)
                 done[b % 2] = ev
             dx, de = dx1, de1
+        def join():  # the side stream's weight gradients are complete before their reduction
+            if conc:
+                nat.check(L.mgn_set_grid_cus(0, 0))
+                for ev in done:
+                    if ev is not None:
+                        main.wait_event(ev)
+
         if defer and GRAD_READY is None and not defer_dense:
+            join()
             nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
         if overlap:
             for ev in done:
@@ -709,6 +766,7 @@ class EPDFunction(torch.autograd.Function):
                 _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
                                   nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
                                   ctypes.pointer(dreds[2]), st)
+                join()
                 # ONE reduction for the whole model: decoder, every processor block, encoders
                 allr = (nat.WgradReduce * (3 + (2 * nb if defer else 0)))()
                 allr[0] = dreds[0]

@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 12
+#define MGN_ABI_VERSION 13
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -252,6 +252,13 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
 #define MGN_BWD_DE_PAIR 2
 #define MGN_BWD_DX_OUT_PAIR 4
 #define MGN_BWD_DX_PAIR 8
+/* ABI v13: the same call split in two halves over the same arguments (keep != NULL): DATA_ONLY runs
+ * the data gradients (dx, de, and what the weight gradients read: dZ saves in `ws`, partials in
+ * `keep`); WGRAD_ONLY then runs the block's single weight-gradient launch and fills reduce2. The
+ * WGRAD_ONLY call may be issued on another stream (ordered after DATA_ONLY by the caller) and run
+ * beside the next block's DATA_ONLY call on ANOTHER workspace; mgn_set_grid_cus gives each its CUs. */
+#define MGN_BWD_DATA_ONLY 16
+#define MGN_BWD_WGRAD_ONLY 32
 int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
                                  const void* x, const void* e, const mgn_block_saved* saved,
                                  const void* dx_out, const void* de_out, void* dx, void* de,
@@ -259,6 +266,12 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
                                  void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                  int32_t flags, mgn_stream_t stream);
 int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream);
+/* ABI v13: caps on the CUs the persistent grids of later launches are sized for (0 = the whole
+ * device): data_cus for every launch except the weight-gradient launches, wgrad_cus for those. Host
+ * state of the library, read when a launch is issued (a captured hipGraph keeps the grids it
+ * recorded); the results do not depend on the caps except for the weight-gradient slab partition
+ * (summation order of the fp32 reductions). */
+int mgn_set_grid_cus(int32_t data_cus, int32_t wgrad_cus);
 /* ABI v12: mgn_mlp_backward (the encoders / decoder of processors.py:71-109, 129-137) with the
  * reduction deferred like mgn_block_backward_deferred: the RMSNorm-scale partials and weight-gradient
  * slabs go to `keep` (mgn_mlp_backward_keep_bytes, alive until the reduction) and *reduce1 describes

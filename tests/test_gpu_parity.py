@@ -678,19 +678,27 @@ def test_training_matches_golden_losses_fp32():
     np.testing.assert_allclose(losses, z["cfgA/losses"], rtol=1e-4)
 
 
-def test_captured_step_equals_eager_step():
+@pytest.mark.parametrize("conc", ["auto", "0,0", "160,96"])
+def test_captured_step_equals_eager_step(conc):
+    """conc: the processor backward's weight gradients on a side stream (MGN_CONC_WGRAD), captured
+    into the hipGraph with its fork / join events."""
+    from graphphysics.models import _engine
     from graphphysics.training.step import TrainStep
 
     res = []
-    for graph in (False, True):
-        sim, opt, sch, data = _cyl_train_setup(torch.float32)
-        st = TrainStep(sim, opt, sch, data, graph=graph)
-        # capture()'s eager warm-up steps are undone: 5 calls = 5 reference updates either way
-        losses = [float(st().item()) for _ in range(5)]
-        torch.cuda.synchronize()
-        res.append((losses, [p.detach().clone() for p in sim.parameters()],
-                    [b.detach().clone() for b in sim.buffers()], opt.param_groups[0]["step_count"],
-                    sch.last_epoch, opt.param_groups[0]["lr"]))
+    _engine.CONC_WGRAD = conc
+    try:
+        for graph in (False, True):
+            sim, opt, sch, data = _cyl_train_setup(torch.float32)
+            st = TrainStep(sim, opt, sch, data, graph=graph)
+            # capture()'s eager warm-up steps are undone: 5 calls = 5 reference updates either way
+            losses = [float(st().item()) for _ in range(5)]
+            torch.cuda.synchronize()
+            res.append((losses, [p.detach().clone() for p in sim.parameters()],
+                        [b.detach().clone() for b in sim.buffers()], opt.param_groups[0]["step_count"],
+                        sch.last_epoch, opt.param_groups[0]["lr"]))
+    finally:
+        _engine.CONC_WGRAD = "auto"
     np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6)
     for a, b in zip(res[0][1], res[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
@@ -1135,3 +1143,46 @@ def test_deferred_weight_gradient_reduction_is_bitwise_identical():
     for other in grads[1:]:
         for a, c in zip(grads[0], other):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("dtype,caps,batch", [(torch.bfloat16, "160,96", 8), (torch.bfloat16, "0,0", 2),
+                                              (torch.float32, "0,0", 2)])
+def test_concurrent_weight_gradients_match_one_stream(dtype, caps, batch):
+    """The processor backward with each block's weight-gradient launch on a side stream beside the
+    next block's data gradients (MGN_BWD_DATA_ONLY / _WGRAD_ONLY, mgn_set_grid_cus caps) computes the
+    same backward as one stream: input gradients bit-identical (every data-gradient kernel works per
+    tile, whatever its grid); parameter gradients bit-identical when the weight-gradient launch keeps
+    the whole chip (caps 0,0: same slab partition), else equal up to the fp32 summation order of the
+    slab / RMSNorm-scale partial reductions (rel-L2 1e-6)."""
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(batch, jitter=0.01)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(b["x"].shape[0], 11, generator=gen).to(DEV).requires_grad_(True)
+    ea = torch.from_numpy(b["edge_attr"]).to(DEV).requires_grad_(True)
+    g = Data(x=x, edge_index=torch.from_numpy(b["edge_index"]).to(DEV), edge_attr=ea)
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(4, 11, 3, 2, 128, compute_dtype=dtype).to(DEV)
+    runs = []
+    for v in ("0", caps):
+        _engine.CONC_WGRAD = v
+        try:
+            y = m(g)
+            y.backward(torch.ones_like(y))
+            torch.cuda.synchronize()
+            runs.append((y.detach().clone(), x.grad.clone(), ea.grad.clone(), [p.grad.clone() for p in m.parameters()]))
+            m.zero_grad(set_to_none=True)
+            x.grad = ea.grad = None
+        finally:
+            _engine.CONC_WGRAD = "auto"
+    (y0, gx0, ge0, p0), (y1, gx1, ge1, p1) = runs
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1) and torch.equal(ge0, ge1)
+    for a, c in zip(p0, p1):
+        if caps == "0,0":
+            assert torch.equal(a, c)
+        else:
+            assert relerr(c, a) <= 1e-6, relerr(c, a)
