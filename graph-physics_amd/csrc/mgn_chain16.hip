@@ -67,6 +67,7 @@ constexpr size_t LDS_VF = (size_t)5 * H * 4, LDS_VB = (size_t)H * 4;
 constexpr size_t lds_fwd(int nwk) { return LDS_W + LDS_VF + (size_t)nwk * SROWS * SLD * 2; }
 constexpr size_t lds_bwd(int nwk) { return LDS_W + LDS_VB + (size_t)nwk * SROWS * SLD * 2 + (size_t)nwk * H * 4; }
 static_assert(lds_bwd(12) <= 163840, "12-wave edge backward exceeds 160 KiB of LDS");
+static_assert(SROWS * SLD * 2 >= 64 * 32, "a wave scratch holds half a 16-row bf16 B operand (partner hand-offs)");
 
 // Diagnostics (build with -DMGN_STAMPS, e.g. MGN_STAMPS=1 python __graft_entry__.py): per-phase
 // s_memtime deltas of wave 0 of workgroup 0, printed once per launch. Not in normal builds.
@@ -86,10 +87,25 @@ static_assert(lds_bwd(12) <= 163840, "12-wave edge backward exceeds 160 KiB of L
     if (blockIdx.x == 0 && threadIdx.x == 0)                                                            \
     printf("%s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", name, st_ph[0], st_ph[1],  \
            st_ph[2], st_ph[3], st_ph[4], st_ph[5], st_ph[6], st_ph[7], st_ph[8], st_ph[9], st_ph[10], st_ph[11])
+// per-wave start / end (s_memrealtime, 100 MHz, one clock for the whole device) of the last launch
+// of each chained kernel kind, read back by mgn_debug_wave_times (the launch's spread of wave ends)
+__device__ unsigned long long g_wave_t[4][4096][2];
+#define WAVE_T0 const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime()
+#define WAVE_REC(k)                                                                                     \
+    do {                                                                                                \
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();                                \
+        const int wi = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                            \
+        if ((threadIdx.x & 63) == 0 && wi < 4096) {                                                    \
+            g_wave_t[k][wi][0] = wave_t0;                                                              \
+            g_wave_t[k][wi][1] = t1;                                                                   \
+        }                                                                                               \
+    } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_PRINT(name)
+#define WAVE_T0
+#define WAVE_REC(k)
 #endif
 
 __device__ __forceinline__ f4 mfma16(const bf16x8& a, const bf16x8& b, const f4& c) {
@@ -466,6 +482,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     int64_t tile = (int64_t)blockIdx.x * NWK + wave;
     const int64_t last = a.ntiles - 1;
     STAMP_DECL;
+    WAVE_T0;
     In16 nxt;
     int di, dj;
     load_idx(a, min(tile, last), lane, di, dj);
@@ -558,6 +575,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         STAMP(7);
     }
     STAMP_PRINT("fwd16");
+    WAVE_REC(0);
 }
 
 // ------------------------------------------------------------------------------------ backward
@@ -633,6 +651,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     int64_t tile = (int64_t)blockIdx.x * NWK + wave;
     const int64_t last = a.ntiles - 1;
     STAMP_DECL;
+    WAVE_T0;
     constexpr bool PGA = NWK < 12;  // three waves per SIMD: the gather is not prefetched (VGPR cap)
     const int gi0 = bidx(a, min(tile, last), lane);
     int gcur = gi0;
@@ -747,6 +766,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         STAMP(8);
     }
     STAMP_PRINT("bwd16");
+    WAVE_REC(1);
     // dscale partials of the workgroup: the waves' rows in wave order
     __syncthreads();
     if (threadIdx.x < H) {
@@ -818,10 +838,12 @@ __device__ __forceinline__ void gemm16_layer0(f4 (&acc)[8], const __bf16* W, con
 // The next block's node projections P = [x·W0bᵀ + b0 ‖ x·W0cᵀ] of node tile `tile`, by a wave other
 // than the one that computed x_out (chain16_node_fwd_kernel's hand-off): half 0's 32 weight fragments
 // (k-steps 4..7 of the next edge MLP's layer-0 pack) are loaded BEFORE waiting for the tile, half
-// 1's stream in under half 0's MFMAs. The x_out rows are read with agent-scope loads (from L2: the
-// producing wave's stores completed before it set *flag).
-__device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int64_t tile, unsigned* flag, __bf16* scr,
-                                               int lane) {
+// 1's stream in under half 0's MFMAs. x_out's bf16 B operand (the bits the tile wave stores) comes
+// through LDS: k-steps 0-1 from the tile wave's scratch, 2-3 from this wave's own (round 4: instead of
+// re-reading the stored x_out rows from L2 after the tile wave waited for its stores to complete —
+// node forward 27.0 -> see DESIGN.md).
+__device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int64_t tile, unsigned* flag,
+                                                  const __bf16* tscr, __bf16* scr, int lane) {
     const int g = lane >> 4;
     const __amdgpu_buffer_rsrc_t rs = gfrag_rsrc(a.pn_pack);
     const int vo = gfrag_voff(lane), kst = a.pn_kst;
@@ -832,16 +854,11 @@ __device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int
         for (int t = 0; t < 8; ++t) fr[s][t] = gfrag<64>(rs, vo, t * kst + 4 + s);
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(2);
     // B operand of x_out rows (as load_e): lane (m, g), k-step s: features 32s + 4g.. and 32s + 16 + 4g..
-    const int64_t row = clamp_row(tile * TR + (lane & 15), a.M);
-    const unsigned long long* xr = reinterpret_cast<const unsigned long long*>(a.out + row * H + 4 * g);
-    bf16x8 Bx[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const unsigned long long lo = __hip_atomic_load(xr + 8 * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long hi = __hip_atomic_load(xr + 8 * s + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32x4 w = {(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
-        Bx[s] = __builtin_bit_cast(bf16x8, w);
-    }
+    const bf16x8* h0 = reinterpret_cast<const bf16x8*>(tscr);
+    const bf16x8* h1 = reinterpret_cast<const bf16x8*>(scr);
+    const bf16x8 Bx[4] = {h0[2 * lane], h0[2 * lane + 1], h1[2 * lane], h1[2 * lane + 1]};
+    lds_fence();  // (own scratch reads back before store_rows reuses it)
+    (void)g;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         f4 pacc[8];
@@ -948,6 +965,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     bf16x8 xb[4];
     f4 agg[8];
     STAMP_DECL;
+    WAVE_T0;
     if (split) {
         if (threadIdx.x < NW / 2) flags[threadIdx.x] = 0u;
         if (wave >= NW / 2) {
@@ -974,7 +992,8 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
     if (handoff && wave >= NW / 2) {
         const int pw = wave - NW / 2;
         const int64_t pt = (int64_t)pw * gridDim.x + blockIdx.x;  // the partner's (only) tile
-        if (pt < a.ntiles) node_proj_partner(a, pt, flags + pw, scr, lane);
+        if (pt < a.ntiles) node_proj_partner(a, pt, flags + pw, scr - (NW / 2) * SROWS * SLD, scr, lane);
+        WAVE_REC(2);
         return;
     }
     for (const int64_t first = tile; tile < a.ntiles; tile += stride) {
@@ -1036,8 +1055,17 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
         if (handoff) {
-            // x_out stores complete (at L2) before the partner is told to read them back
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // x_out's bf16 B operand to the partner through LDS: k-steps 0-1 in this wave's scratch
+            // (free again after store_rows), 2-3 in the partner's (idle until it has read them)
+            bf16x8 Bx[4];
+            to_operand(acc, Bx);
+            bf16x8* h0 = reinterpret_cast<bf16x8*>(scr);
+            bf16x8* h1 = reinterpret_cast<bf16x8*>(scr + (NW / 2) * SROWS * SLD);
+            h0[2 * lane] = Bx[0];
+            h0[2 * lane + 1] = Bx[1];
+            h1[2 * lane] = Bx[2];
+            h1[2 * lane + 1] = Bx[3];
+            lds_fence();
             if (lane == 0) __hip_atomic_store(flags + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (a.pn_out) {
             // the NEXT block's node projections from this tile's x_out (bf16, the bits just stored):
@@ -1065,6 +1093,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
         STAMP(3);
     }
     STAMP_PRINT("nfwd16");
+    WAVE_REC(2);
 }
 
 // The wave's bf16 B operand (a 16-row tile, k-steps 0..3) as R8 octets 2*tile, 2*tile+1 of dst, through
@@ -1205,6 +1234,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
     u32x2 d[8];
     unsigned mk[3];
     STAMP_DECL;
+    WAVE_T0;
     if (split) {
         if (threadIdx.x < NW / 2) flags[threadIdx.x] = 0u;
         if (wave >= NW / 2)
@@ -1285,6 +1315,7 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_bwd_kernel(ChainNodeBwdA
         STAMP(2);
     }
     STAMP_PRINT("nbwd16");
+    WAVE_REC(3);
     __syncthreads();
     if (threadIdx.x < H) {
         float s2 = 0.f;
@@ -1885,4 +1916,20 @@ int chain16_dense_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv,
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), LDS_TOTAL, st, a);
     MGN_LAUNCH_CHECK();
     return 0;
+}
+
+// Diagnostics (MGN_STAMPS builds only): per-wave [start, end] s_memrealtime ticks (100 MHz) of the last
+// launch of a chained kernel kind (0 edge fwd, 1 edge bwd, 2 node fwd, 3 node bwd), n <= 4096 waves.
+extern "C" int mgn_debug_wave_times(int32_t kind, uint64_t* out, int32_t n) {
+#ifdef MGN_STAMPS
+    if (kind < 0 || kind > 3 || n < 0 || n > 4096) return 1000;
+    (void)hipDeviceSynchronize();
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), (size_t)n * 16, (size_t)kind * 4096 * 16,
+                                    hipMemcpyDeviceToHost);
+#else
+    (void)kind;
+    (void)out;
+    (void)n;
+    return 1000;
+#endif
 }

@@ -27,6 +27,27 @@ namespace {
 
 enum { MODE_DENSE = 0, MODE_EDGE = 1, MODE_NODE = 2 };
 
+#ifdef MGN_STAMPS  // diagnostics builds: per-phase s_memtime deltas of wave 0 of workgroup 0 (as mgn_chain16.hip)
+#define F32C_STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define F32C_STAMP(i)                                                                     \
+    do {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        unsigned long long st_t;                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");     \
+        __builtin_amdgcn_sched_barrier(0);                                                \
+        st_ph[i] += st_t - st_prev;                                                       \
+        st_prev = st_t;                                                                   \
+    } while (0)
+#define F32C_STAMP_PRINT(name)                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                                                     \
+    printf("%s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", name, st_ph[0], st_ph[1], st_ph[2], \
+           st_ph[3], st_ph[4], st_ph[5], st_ph[6], st_ph[7], st_ph[8], st_ph[9], st_ph[10], st_ph[11])
+#else
+#define F32C_STAMP_DECL
+#define F32C_STAMP(i)
+#define F32C_STAMP_PRINT(name)
+#endif
+
 template <int NT, int MT>
 #ifndef MGN_F32_PD
 #define MGN_F32_PD 8  // weight k-steps in flight in the generic fp32 GEMMs (A/B: 4 -> 86.8, 8 -> 90.0, 16 -> 88.5 steps/s)
@@ -105,6 +126,38 @@ struct Gemm {
     __device__ __forceinline__ int n_of(int i) const { return (nt0 + i) * 16 + ((threadIdx.x & 63) >> 4) * 4; }
     __device__ __forceinline__ int m_of(int j) const { return (mt0 + j) * 16 + (threadIdx.x & 15); }
 };
+
+// Weights in LDS (small MLPs, hidden <= 64): every layer's packed fragments the kernel reads (a
+// contiguous prefix of the layer's pack) are copied into LDS by LDS-DMA at kernel start — one round
+// trip that overlaps the input loads — instead of each layer's GEMM streaming them from L2 (which
+// exposed one L2 round trip per 8 k-steps: measured, MGN_STAMPS, fp32 h=32 edge forward: 19.4k of
+// 38k cycles in the GEMMs of layers 0-2). WlDesc: per layer, source element offset in the pack and
+// element count; LDS copies are consecutive (layer l at wl_lo[l] elements).
+struct WlDesc {
+    int32_t n;                      // layers staged (0: weights read from global memory)
+    int32_t pad;
+    int64_t src[MGN_MAX_LAYERS];    // element offset of the layer's prefix in the pack
+    int32_t cnt[MGN_MAX_LAYERS];    // elements
+    int32_t lo[MGN_MAX_LAYERS];     // element offset of its LDS copy
+};
+
+// issue the LDS-DMA copies (all waves; 16 bytes per lane, a wave instruction = 1 KiB); the caller
+// waits vmcnt(0) and barriers before the first read
+template <class T>
+__device__ __forceinline__ void wl_issue(const WlDesc& d, const T* pack, T* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    constexpr int EPL = 16 / sizeof(T);  // elements per lane
+    for (int l = 0; l < d.n; ++l) {
+        const int pieces = (d.cnt[l] + 64 * EPL - 1) / (64 * EPL);
+        for (int pc = wave; pc < pieces; pc += nw) {
+            const int e0 = pc * 64 * EPL;
+            if (e0 + lane * EPL < d.cnt[l])
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(pack + d.src[l] + e0 + lane * EPL),
+                    (__attribute__((address_space(3))) void*)(lds + d.lo[l] + e0), 16, 0, 0);
+        }
+    }
+}
 
 struct SrcSeg {
     const void* p;
@@ -252,6 +305,8 @@ struct FwdArgs {
     float* rden_save;
     int32_t ablate;  // diagnostics builds only (-DMGN_ABLATE=bits): 1 gather, 2 R8 saves, 4 MFMA, 8 epilogue stores
     int32_t r0_elems;  // LDS region 0 (layer-0 input / odd-layer activations / fp32 z staging), in T
+    int32_t wl_elems;  // WL kernels: LDS element offset of the staged weights
+    WlDesc wl;
 };
 
 // Diagnostic ablation mask for timing studies (results are wrong when nonzero): a compile-time
@@ -373,7 +428,7 @@ __device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float*
     }
 }
 
-template <class T, int H, int BM, int MODE>
+template <class T, int H, int BM, int MODE, bool WL = false>
 __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     constexpr int KSTEP = Mf<T>::KSTEP;
     constexpr int NTH = H / 16, MT = BM / 16;
@@ -384,8 +439,11 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     T* P0 = In + a.r0_elems;
     T* P1 = In;  // In is dead after layer 0
     float* red = reinterpret_cast<float*>(P0 + BM * a.ldh);
+    T* Wl = reinterpret_cast<T*>(smem) + a.wl_elems;  // WL: the staged weight prefixes
     const int64_t row0 = (int64_t)blockIdx.x * BM;
 
+    F32C_STAMP_DECL;
+    if (WL) wl_issue<T>(a.wl, reinterpret_cast<const T*>(a.wpack), Wl);
     if (!(a.ablate & 1)) load_tile<T, BM>(In, a.ldi, a.K0, KP0, a.seg, a.nseg, row0, a.M);
     if (MODE == MODE_NODE && !(a.ablate & 1)) {
         // aggregation: In[r][H + c] = sum over in-edges k of scale[c] * (z[k][c] / rden[k])
@@ -427,17 +485,24 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
             Chunk<T>::store(In + (size_t)r * a.ldi + H + c, acc);
         }
     }
+    if (WL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight copies landed
     __syncthreads();
+    F32C_STAMP(0);
     // the layer-0 input of edge/node MLPs is re-gathered by the weight-gradient kernel
     if (MODE == MODE_DENSE && !(a.ablate & 2))
         copy_out_r8<T, BM>(In, a.ldi, KP0, reinterpret_cast<T*>(a.act8) + a.act_off[0], row0);
+    F32C_STAMP(1);
 
     const T* wp = reinterpret_cast<const T*>(a.wpack);
     const T* cur = In;
     int ldc = a.ldi, KS = KP0 / KSTEP, K = a.Kpack0;
     for (int l = 0; l < a.L - 1; ++l) {
         Gemm<T, NTH, MT> g;
-        g.run(wp, KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
+        if (WL)
+            g.run(Wl + a.wl.lo[l], KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
+        else
+            g.run(wp, KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
+        F32C_STAMP(2);
         T* nxt = (l & 1) ? P1 : P0;
         if (g.active) {
             const float* b = a.bias[l];
@@ -475,22 +540,28 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
                 nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
         }
         __syncthreads();
+        F32C_STAMP(3);
         if (!(a.ablate & 2))
             copy_out_r8<T, BM>(nxt, a.ldh, rup(H, KSTEP), reinterpret_cast<T*>(a.act8) + a.act_off[l + 1], row0);
+        F32C_STAMP(4);
         wp += linear_pack_elems(H, K, dtype_id<T>());
         cur = nxt;
         ldc = a.ldh;
         KS = cdiv(H, KSTEP);
         K = H;
     }
+    const T* wlast = WL ? Wl + a.wl.lo[a.L - 1] : wp;
     if (a.NOUT == H) {
         Gemm<T, NTH, MT> g;
-        g.run(wp, KS, cur, ldc, a.ablate & 4);
+        g.run(wlast, KS, cur, ldc, a.ablate & 4);
+        F32C_STAMP(5);
         if (a.ablate & 8) return;
         fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
+        F32C_STAMP(6);
+        F32C_STAMP_PRINT(MODE == MODE_EDGE ? "gfe" : MODE == MODE_NODE ? "gfn" : "gfd");
     } else {
         Gemm<T, 1, MT> g;
-        g.run(wp, KS, cur, ldc);
+        g.run(wlast, KS, cur, ldc);
         fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
     }
 }
@@ -520,9 +591,11 @@ struct BwdArgs {
     int64_t din_ld;
     void* o1;               // EDGE: de_in [M][H]; NODE: dx_part [M][H]  (T)
     void* o2;               // EDGE: dZ_0 [M][H] row-major; NODE: d_aggr [M][H]   (T)
+    int32_t wl_elems;       // WL kernels: LDS element offset of the staged (transposed) weights
+    WlDesc wl;
 };
 
-template <class T, int H, int BM, int MODE>
+template <class T, int H, int BM, int MODE, bool WL = false>
 __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     constexpr int KSTEP = Mf<T>::KSTEP, VEC = Mf<T>::VEC;
     constexpr int NTH = H / 16, MT = BM / 16;
@@ -530,10 +603,12 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     T* D0 = reinterpret_cast<T*>(smem);
     T* D1 = D0 + BM * a.ldh;
     float* red = reinterpret_cast<float*>(D1 + BM * a.ldh);  // [256][4]
+    T* Wl = reinterpret_cast<T*>(smem) + a.wl_elems;
     const int64_t row0 = (int64_t)blockIdx.x * BM;
     const int tid = threadIdx.x;
     const int NO = a.NOUT;
     const int KPN = rup(NO, KSTEP);
+    if (WL) wl_issue<T>(a.wl, reinterpret_cast<const T*>(a.wtpack), Wl);
 
     // ---- dY -> dZ_last (RMSNorm backward), chunks of 4 columns; CPR lanes per row
     {
@@ -625,8 +700,12 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
             }
         }
     }
+    F32C_STAMP_DECL;
+    if (WL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight copies landed
     __syncthreads();
+    F32C_STAMP(0);
     copy_out_r8<T, BM>(D0, a.ldh, H, reinterpret_cast<T*>(a.dz8) + (int64_t)(a.L - 1) * a.RP * H, row0);
+    F32C_STAMP(1);
 
     // ---- layers L-1 .. 1 : dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]
     const T* wt = reinterpret_cast<const T*>(a.wtpack);
@@ -644,7 +723,11 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     for (int l = a.L - 1; l >= 1; --l) {
         const int Nl = l == a.L - 1 ? NO : H;
         Gemm<T, NTH, MT> g;
-        g.run(wt + off[l], cdiv(Nl, KSTEP), cur, a.ldh);
+        if (WL)
+            g.run(Wl + a.wl.lo[l], cdiv(Nl, KSTEP), cur, a.ldh);
+        else
+            g.run(wt + off[l], cdiv(Nl, KSTEP), cur, a.ldh);
+        F32C_STAMP(2);
         if (g.active) {
             const int lane = tid & 63;
 #pragma unroll
@@ -670,10 +753,12 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
                 nxt[(size_t)(it / padc) * a.ldh + H + it % padc] = from_f<T>(0.f);
         }
         __syncthreads();
+        F32C_STAMP(3);
         T* t = cur;
         cur = nxt;
         nxt = t;
         copy_out_r8<T, BM>(cur, a.ldh, H, reinterpret_cast<T*>(a.dz8) + (int64_t)(l - 1) * a.RP * H, row0);
+        F32C_STAMP(4);
     }
 
     // ---- layer 0 : dA0 = dZ_0 · W_0, K0 columns in chunks of H
@@ -693,7 +778,11 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     const int nchunk = cdiv(cdiv(a.K0, 16), NTH);
     for (int c = 0; c < nchunk; ++c) {
         Gemm<T, NTH, MT> g;
-        g.run(wt + off[0] + (int64_t)c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+        if (WL)
+            g.run(Wl + a.wl.lo[0] + c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+        else
+            g.run(wt + off[0] + (int64_t)c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+        F32C_STAMP(5);
         if (MODE != MODE_DENSE) {
             // stage the chunk in the free LDS buffer, then write coalesced 16-byte row chunks
             if (g.active) {
@@ -722,6 +811,8 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
                 }
             }
             __syncthreads();
+            F32C_STAMP(6);
+            if (c == nchunk - 1) F32C_STAMP_PRINT(MODE == MODE_EDGE ? "gbe" : "gbn");
             continue;
         }
         if (!g.active) continue;
@@ -783,6 +874,16 @@ struct WgArgs {
 // combine their tiles through LDS in a fixed order: twice the resident waves of a 4-wave
 // workgroup without more partial slabs.
 constexpr int WG_GROUPS = 2;
+// k-steps of R8 operands in flight in the weight-gradient kernel's direct (fp32) path (A/B builds:
+// 0 = two, by unrolling) and workgroups per CU of its h <= 32 launches. Measured (Cfg A, fp32 h=32,
+// weight-gradient launch per block): 2-deep / 4 per CU 30.7 us, 8-deep / 2 per CU 24.8 us (1,556 ->
+// 1,611 steps/s), 8 / 1 38.1, 4 / 4 31.1, 16 / 1 45.1
+#ifndef MGN_WG_PF
+#define MGN_WG_PF 8
+#endif
+#ifndef MGN_WG_PER_CU32
+#define MGN_WG_PER_CU32 2
+#endif
 
 template <class T, int H>
 size_t wgrad_lds_bytes(bool staged) {
@@ -804,6 +905,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int grp = threadIdx.x / MGN_THREADS, tid = threadIdx.x % MGN_THREADS;
     T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * H * LDT;  // this group's [2][H][LDT]
+    F32C_STAMP_DECL;
     const WgJob job = a.job[blockIdx.y];
     const bool multi = a.multi != 0;
     if (multi && (int)blockIdx.x >= job.nchunks) return;  // uniform per workgroup, before any barrier
@@ -930,6 +1032,44 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 return ld_frag(reinterpret_cast<const T*>(buf + (ks * (KSTEP / 8) + (lane >> 4)) * H + (mt0 + j) * 16 +
                                                           (lane & 15)));
             });
+    } else if (!staged && MGN_WG_PF > 0) {
+        // R8 operands straight from global memory (fp32: one VGPR per fragment): a register ring
+        // keeps MGN_WG_PF k-steps of both operands in flight (the loop is unrolled by it so every
+        // slot is static; loads past the chunk clamp to its first k-step and are never consumed).
+        // Same MFMA sequence as one k-step at a time: bit-identical sums.
+        constexpr int PF = MGN_WG_PF > 0 ? MGN_WG_PF : 1;
+        constexpr int64_t STEP = (int64_t)WG_GROUPS * KSTEP;
+        typename Mf<T>::frag ra[PF][C::NTW], rb[PF][C::MTW];
+        auto load = [&](int64_t m0, typename Mf<T>::frag (&fa)[C::NTW], typename Mf<T>::frag (&fb)[C::MTW]) {
+            const int64_t mr = (m0 < r_end ? m0 : r_begin) + VEC * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j)
+                fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
+        };
+        const int64_t m_first = r_begin + grp * KSTEP;
+        if (active && m_first < r_end) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) load(m_first + u * STEP, ra[u], rb[u]);
+            for (int64_t m0 = m_first; m0 < r_end; m0 += PF * STEP) {
+#pragma unroll
+                for (int u = 0; u < PF; ++u) {
+                    if (m0 + u * STEP >= r_end) break;
+                    typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i) fa[i] = ra[u][i];
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) fb[j] = rb[u][j];
+                    load(m0 + (u + PF) * STEP, ra[u], rb[u]);
+#pragma unroll
+                    for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                        for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
+                    if (do_bias) bias_acc(fa);
+                }
+            }
+        }
     } else if (!staged) {
 #pragma unroll 2
         for (int64_t m0 = r_begin + grp * KSTEP; m0 < r_end; m0 += WG_GROUPS * KSTEP) {
@@ -1039,6 +1179,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 return ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
             });
     }
+    F32C_STAMP(0);
     // Combine and store through a canonical [n][k] tile in LDS (row pitch H+4 floats: the four
     // 16-lane groups of an accumulator write land 16 banks apart): group 1 deposits its tile,
     // group 0 adds its own, then all 512 threads store the slab rows with coalesced 16-byte stores
@@ -1093,6 +1234,8 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
         }
     }
     if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
+    F32C_STAMP(1);
+    if (blockIdx.y == 0) F32C_STAMP_PRINT("gwg");
 }
 
 // Ring variant for bf16 h=128 (the hot configuration): the whole workgroup (8 waves as 4 n-groups
@@ -1628,26 +1771,6 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 // 186); the same with 4-wave workgroups spilled 200+ bytes per lane.
 #ifndef MGN_F32_CHAIN
 #define MGN_F32_CHAIN 1  // 0: the fp32 edge MLP on the generic LDS-tiled kernels (A/B builds)
-#endif
-#ifdef MGN_STAMPS  // diagnostics builds: per-phase s_memtime deltas of wave 0 of workgroup 0 (as mgn_chain16.hip)
-#define F32C_STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
-#define F32C_STAMP(i)                                                                     \
-    do {                                                                                  \
-        __builtin_amdgcn_sched_barrier(0);                                                \
-        unsigned long long st_t;                                                          \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t)::"memory");     \
-        __builtin_amdgcn_sched_barrier(0);                                                \
-        st_ph[i] += st_t - st_prev;                                                       \
-        st_prev = st_t;                                                                   \
-    } while (0)
-#define F32C_STAMP_PRINT(name)                                                                                   \
-    if (blockIdx.x == 0 && threadIdx.x == 0)                                                                     \
-    printf("%s %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", name, st_ph[0], st_ph[1], st_ph[2], \
-           st_ph[3], st_ph[4], st_ph[5], st_ph[6], st_ph[7], st_ph[8], st_ph[9], st_ph[10], st_ph[11])
-#else
-#define F32C_STAMP_DECL
-#define F32C_STAMP(i)
-#define F32C_STAMP_PRINT(name)
 #endif
 #ifndef MGN_F32C_SB
 #define MGN_F32C_SB 0  // 1: single-buffered images, 6-wave workgroups, two workgroups per CU (A/B builds)
@@ -2186,8 +2309,36 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
     if (zb > r0) r0 = zb;
     r0 = (r0 + 15) / 16 * 16;
     a.r0_elems = (int)(r0 / sizeof(T));
-    const size_t lds = r0 + (size_t)BM * a.ldh * sizeof(T) + 4 * BM * sizeof(float);
-    auto fn = mlp_fwd_kernel<T, H, BM, MODE>;
+    size_t lds = r0 + (size_t)BM * a.ldh * sizeof(T) + 4 * BM * sizeof(float);
+    // weights in LDS: the fragment prefix each layer's GEMM reads (layer 0 only when its k-steps are
+    // contiguous: no split layer 0 reading the e block of a wider pack)
+    bool wl = false;
+    if (H <= 64 && a.kstride0 == rup(a.K0, Mf<T>::KSTEP) / Mf<T>::KSTEP && !a.ablate) {
+        constexpr int FE = 64 * Mf<T>::VEC;  // elements per fragment
+        int64_t src = 0, lo = 0;
+        for (int l = 0; l < a.L; ++l) {
+            int n, k;
+            mlp_layer_shape(*m, l, &n, &k);
+            const int ks = l == 0 ? a.kstride0 : cdiv(H, Mf<T>::KSTEP);
+            const int nt = (l == a.L - 1 && a.NOUT != H) ? 1 : H / 16;
+            a.wl.src[l] = src;
+            a.wl.cnt[l] = nt * ks * FE;
+            a.wl.lo[l] = (int32_t)lo;
+            lo += a.wl.cnt[l];
+            src += linear_pack_elems(n, k, dtype_id<T>());
+        }
+        a.wl.n = a.L;
+        const size_t wb = (size_t)lo * sizeof(T);
+        if (wb <= 48 * 1024) {
+            lds = (lds + 15) / 16 * 16;
+            a.wl_elems = (int32_t)(lds / sizeof(T));
+            lds += wb;
+            wl = true;
+        } else {
+            a.wl.n = 0;
+        }
+    }
+    auto fn = wl ? mlp_fwd_kernel<T, H, BM, MODE, true> : mlp_fwd_kernel<T, H, BM, MODE, false>;
     if (int e = set_lds((const void*)fn, lds)) return e;
     const int grid = (int)(rows_pad(M) / BM);
     if (grid == 0) return 0;
@@ -2258,8 +2409,37 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
             return 0;
         }
     }
-    const size_t lds = 2 * (size_t)BM * a.ldh * sizeof(T) + MGN_THREADS * 4 * sizeof(float);
-    auto fn = mlp_bwd_kernel<T, H, BM, MODE>;
+    size_t lds = 2 * (size_t)BM * a.ldh * sizeof(T) + MGN_THREADS * 4 * sizeof(float);
+    // weights in LDS (as launch_fwd): the transposed-fragment prefix each layer's GEMM reads
+    bool wl = false;
+    if (H <= 64) {
+        constexpr int FE = 64 * Mf<T>::VEC;
+        const int NO = a.NOUT;
+        int64_t src = 0, lo = 0;
+        const int nchunk = (MODE == MODE_DENSE && o.din == nullptr) ? 0 : cdiv(cdiv(a.K0, 16), H / 16);
+        for (int l = 0; l < a.L; ++l) {
+            int n, k;
+            mlp_layer_shape(*m, l, &n, &k);
+            const int Nl = l == a.L - 1 ? NO : H;
+            a.wl.src[l] = src;
+            a.wl.cnt[l] = l == 0 ? nchunk * (H / 16) * cdiv(a.L == 1 ? NO : H, Mf<T>::KSTEP) * FE
+                                 : (H / 16) * cdiv(Nl, Mf<T>::KSTEP) * FE;
+            a.wl.lo[l] = (int32_t)lo;
+            lo += a.wl.cnt[l];
+            src += linear_pack_elems(n, k, dtype_id<T>());
+        }
+        a.wl.n = a.L;
+        const size_t wb = (size_t)lo * sizeof(T);
+        if (wb <= 48 * 1024) {
+            lds = (lds + 15) / 16 * 16;
+            a.wl_elems = (int32_t)(lds / sizeof(T));
+            lds += wb;
+            wl = true;
+        } else {
+            a.wl.n = 0;
+        }
+    }
+    auto fn = wl ? mlp_bwd_kernel<T, H, BM, MODE, true> : mlp_bwd_kernel<T, H, BM, MODE, false>;
     if (int e = set_lds((const void*)fn, lds)) return e;
     const int grid = (int)(rows_pad(M) / BM);
     if (grid == 0) return 0;
@@ -2293,7 +2473,7 @@ int64_t wgrad_max_chunks(int64_t RP, int H = 128) {
     if (c > cap) c = cap;
     return c < 1 ? 1 : c;
 }
-int wgrad_wgs_per_cu(int H) { return H <= 32 ? 4 : 1; }
+int wgrad_wgs_per_cu(int H) { return H <= 32 ? MGN_WG_PER_CU32 : 1; }
 int wgrad_rows_per_chunk(int64_t RP, int njobs, int H = 128) {
     int64_t chunks = (int64_t)wgrad_wgs_per_cu(H) * wgrad_cus() / njobs;
     const int64_t cap = wgrad_max_chunks(RP, H);

@@ -112,6 +112,7 @@ EXPORTS = {
                                             _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_wgrad_reduce_many": (_i32, [ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_set_grid_cus": (_i32, [_i32, _i32]),
+    "mgn_debug_wave_times": (_i32, [_i32, _vp, _i32]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
     "mgn_column_stats_workspace_bytes": (_sz, [_i64, _i32]),

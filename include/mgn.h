@@ -272,6 +272,10 @@ int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t 
  * recorded); the results do not depend on the caps except for the weight-gradient slab partition
  * (summation order of the fp32 reductions). */
 int mgn_set_grid_cus(int32_t data_cus, int32_t wgrad_cus);
+/* Diagnostics builds (MGN_STAMPS) only, else an error status: per-wave [start, end] s_memrealtime ticks
+ * (100 MHz) of the last launch of a chained kernel kind (0 edge fwd, 1 edge bwd, 2 node fwd, 3 node
+ * bwd), n <= 4096 waves in workgroup-major order. */
+int mgn_debug_wave_times(int32_t kind, uint64_t* out, int32_t n);
 /* ABI v12: mgn_mlp_backward (the encoders / decoder of processors.py:71-109, 129-137) with the
  * reduction deferred like mgn_block_backward_deferred: the RMSNorm-scale partials and weight-gradient
  * slabs go to `keep` (mgn_mlp_backward_keep_bytes, alive until the reduction) and *reduce1 describes

@@ -34,7 +34,7 @@ def sources_sha():
 def kernel_class(name):
     """bench.py / libmgn profiler class of a kernel instance (None: not a training-step class)."""
     # generic MLP kernels, mangled (..._kernelIfLi128ELi32ELi1E...) or demangled (<float, 128, 32, 1>)
-    m = re.search(r"mlp_(fwd|bwd)_kernel(?:.*?Li(\d+)ELi(\d+)ELi(\d)E|<[^,<>]+, (\d+), (\d+), (\d)>)", name)
+    m = re.search(r"mlp_(fwd|bwd)_kernel(?:.*?Li(\d+)ELi(\d+)ELi(\d)E|<[^,<>]+, (\d+), (\d+), (\d)(?:, (?:true|false))?>)", name)
     if m:
         mode = m.group(4) or m.group(7)
         return f"{m.group(1)}_" + {"0": "dense", "1": "edge", "2": "node"}[mode]
