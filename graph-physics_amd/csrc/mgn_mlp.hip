@@ -123,6 +123,45 @@ struct Gemm {
             }
         }
     }
+    // The same GEMM with the weight fragments in LDS (WL kernels): groups of G k-steps whose A and B
+    // fragments are all read before the group's MFMAs (one LDS round trip per group instead of one per
+    // k-step: the runtime-KS loop above compiled to read -> wait -> MFMA per k-step, ~200 cycles each).
+    // Same MFMA sequence per accumulator (k-steps ascending): bit-identical to run().
+    __device__ __forceinline__ void run_lds(const T* wp, int KS, const T* lds, int ldl, int kstride = 0) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int wn = wave % C::WN, wm = wave / C::WN;
+        nt0 = wn * C::NTW;
+        mt0 = wm * C::MTW;
+        active = mt0 < MT;
+#pragma unroll
+        for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+            for (int j = 0; j < C::MTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        if (!active) return;
+        if (kstride <= 0) kstride = KS;
+        const T* bp = lds + (size_t)(mt0 * 16 + (lane & 15)) * ldl + VEC * (lane >> 4);
+        const T* ap = wp + ((size_t)nt0 * kstride * 64 + lane) * VEC;
+        constexpr int G = sizeof(T) == 4 ? 8 : 4;
+        for (int k0 = 0; k0 < KS; k0 += G) {
+            typename Mf<T>::frag a[G][C::NTW], b[G][C::MTW];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const int ks = k0 + u < KS ? k0 + u : KS - 1;
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i) a[u][i] = ld_frag(ap + ((size_t)i * kstride + ks) * 64 * VEC);
+#pragma unroll
+                for (int j = 0; j < C::MTW; ++j) b[u][j] = ld_frag(bp + (size_t)j * 16 * ldl + ks * KSTEP);
+            }
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                if (k0 + u >= KS) break;
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(a[u][i], b[u][j], acc[i][j]);
+            }
+        }
+    }
     __device__ __forceinline__ int n_of(int i) const { return (nt0 + i) * 16 + ((threadIdx.x & 63) >> 4) * 4; }
     __device__ __forceinline__ int m_of(int j) const { return (mt0 + j) * 16 + (threadIdx.x & 15); }
 };
@@ -499,7 +538,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     for (int l = 0; l < a.L - 1; ++l) {
         Gemm<T, NTH, MT> g;
         if (WL)
-            g.run(Wl + a.wl.lo[l], KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
+            g.run_lds(Wl + a.wl.lo[l], KS, cur, ldc, l == 0 ? a.kstride0 : KS);
         else
             g.run(wp, KS, cur, ldc, a.ablate & 4, l == 0 ? a.kstride0 : KS);
         F32C_STAMP(2);
@@ -553,7 +592,10 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     const T* wlast = WL ? Wl + a.wl.lo[a.L - 1] : wp;
     if (a.NOUT == H) {
         Gemm<T, NTH, MT> g;
-        g.run(wlast, KS, cur, ldc, a.ablate & 4);
+        if (WL)
+            g.run_lds(wlast, KS, cur, ldc);
+        else
+            g.run(wlast, KS, cur, ldc, a.ablate & 4);
         F32C_STAMP(5);
         if (a.ablate & 8) return;
         fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
@@ -561,7 +603,10 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
         F32C_STAMP_PRINT(MODE == MODE_EDGE ? "gfe" : MODE == MODE_NODE ? "gfn" : "gfd");
     } else {
         Gemm<T, 1, MT> g;
-        g.run(wlast, KS, cur, ldc);
+        if (WL)
+            g.run_lds(wlast, KS, cur, ldc);
+        else
+            g.run(wlast, KS, cur, ldc);
         fwd_last_epilogue<T, BM>(g, a, red, reinterpret_cast<float*>(In), row0);
     }
 }
@@ -724,7 +769,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
         const int Nl = l == a.L - 1 ? NO : H;
         Gemm<T, NTH, MT> g;
         if (WL)
-            g.run(Wl + a.wl.lo[l], cdiv(Nl, KSTEP), cur, a.ldh);
+            g.run_lds(Wl + a.wl.lo[l], cdiv(Nl, KSTEP), cur, a.ldh);
         else
             g.run(wt + off[l], cdiv(Nl, KSTEP), cur, a.ldh);
         F32C_STAMP(2);
@@ -779,7 +824,7 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
     for (int c = 0; c < nchunk; ++c) {
         Gemm<T, NTH, MT> g;
         if (WL)
-            g.run(Wl + a.wl.lo[0] + c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
+            g.run_lds(Wl + a.wl.lo[0] + c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
         else
             g.run(wt + off[0] + (int64_t)c * NTH * KS0 * 64 * VEC, KS0, cur, a.ldh);
         F32C_STAMP(5);
