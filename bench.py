@@ -228,21 +228,33 @@ def warm(a, step):
     torch.cuda.synchronize()
 
 
+PROFILE_SCHEDULE = ("one stream, whole chip: each kernel class timed alone (the timed replay runs the "
+                    "processor's weight-gradient launches on a side stream beside the data gradients, each on "
+                    "its share of the CUs)")
+
+
 def profile_classes(a, step):
     """Per-kernel-class durations: HIP events on the launch stream around every kernel of K steps run
-    eagerly (the same kernels, shapes and launch order the replayed graph contains), after two
-    unprofiled eager steps (the first eager step after replays pays one-time costs)."""
+    eagerly (the same kernels and shapes the replayed graph contains), after two unprofiled eager steps
+    (the first eager step after replays pays one-time costs). On ONE stream (PROFILE_SCHEDULE): a
+    kernel's roofline is its own, not its share of a chip it splits with a concurrent launch."""
     from graphphysics import _native as nat
+    from graphphysics.models import _engine
 
-    for _ in range(2):
-        step.eager()
-    torch.cuda.synchronize()
-    nat.profile_enable(True)
-    for _ in range(a.steps):
-        step.eager()
-    torch.cuda.synchronize()
-    prof = nat.profile_collect()
-    nat.profile_enable(False)
+    saved = _engine.CONC_WGRAD
+    _engine.CONC_WGRAD = "0"
+    try:
+        for _ in range(2):
+            step.eager()
+        torch.cuda.synchronize()
+        nat.profile_enable(True)
+        for _ in range(a.steps):
+            step.eager()
+        torch.cuda.synchronize()
+        prof = nat.profile_collect()
+        nat.profile_enable(False)
+    finally:
+        _engine.CONC_WGRAD = saved
     return prof
 
 
@@ -506,7 +518,7 @@ def main():
                    "global_batch": (a.batch if a.workload == "cylinder" else 1) * world,
                    "parallelism": "dp%d" % world,
                    "graphs_per_sec": round(value * gpb, 2)},
-        "roofline": roof, "kernels": kinds, "last_loss": last_loss,
+        "roofline": roof, "kernels": kinds, "kernels_schedule": PROFILE_SCHEDULE, "last_loss": last_loss,
     }
     if dp_info is not None:
         out["data_parallel"] = dp_info
