@@ -93,6 +93,17 @@ PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
 # workspaces), each on its own share of the CUs (mgn_set_grid_cus). MGN_CONC_WGRAD: "auto" (default:
 # conc_caps below), "0" (one stream), or "data_cus,wgrad_cus" (0,0: both streams uncapped).
 CONC_WGRAD = os.environ.get("MGN_CONC_WGRAD", "auto")
+# concurrent backward: workspaces rotated between blocks (MGN_CONC_WS = count or "all" = one per block).
+# The data half of block b waits for the weight gradients of block b + count before reusing a workspace,
+# which keeps the two streams in lock-step: the ring then reads each block's dZ saves right after they
+# were written, from the Infinity Cache (measured: "all" lets the data half run ahead, the saves are
+# evicted before the ring reads them and the step slows 337 -> 311 steps/s)
+CONC_WS = os.environ.get("MGN_CONC_WS", "2")
+# concurrent backward: each block's slab reduction on the side stream right after its weight-gradient
+# launch instead of in the one reduction launch at the end of the backward (same sums; measured Cfg B
+# 344.1 -> 345.1 steps/s, sustained 352.3 -> 354.6: the end-of-backward reduction leaves the critical
+# path). MGN_SIDE_REDUCE=0: one reduction at the end
+SIDE_REDUCE = os.environ.get("MGN_SIDE_REDUCE", "1") == "1"
 
 
 def conc_caps(E, chained):
@@ -667,8 +678,9 @@ class EPDFunction(torch.autograd.Function):
         if conc:
             main = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
-            wss = [torch.empty_like(ws), torch.empty_like(ws)]
-            done = [None, None]
+            nws = nb if CONC_WS == "all" else max(int(CONC_WS), 2)
+            wss = [torch.empty_like(ws) for _ in range(nws)]
+            done = [None] * nws
             nat.check(L.mgn_set_grid_cus(*caps))
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
@@ -686,9 +698,9 @@ class EPDFunction(torch.autograd.Function):
                 if b > 0:
                     flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
             if conc:
-                w = wss[b % 2]
-                if done[b % 2] is not None:
-                    main.wait_event(done[b % 2])  # the side stream is done reading this workspace
+                w = wss[b % nws]
+                if done[b % nws] is not None:
+                    main.wait_event(done[b % nws])  # the side stream is done reading this workspace
                 kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
                                                          flags | nat.MGN_BWD_DATA_ONLY, st))
@@ -697,9 +709,11 @@ class EPDFunction(torch.autograd.Function):
                 side.wait_event(ev)
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
                                                          flags | nat.MGN_BWD_WGRAD_ONLY, nat._vp(side.cuda_stream)))
+                if SIDE_REDUCE:
+                    nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2, nat._vp(side.cuda_stream)))
                 ev = torch.cuda.Event()
                 ev.record(side)
-                done[b % 2] = ev
+                done[b % nws] = ev
             elif defer:
                 nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
                                                          ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
@@ -741,9 +755,11 @@ class EPDFunction(torch.autograd.Function):
                     if ev is not None:
                         main.wait_event(ev)
 
+        side_reduced = conc and SIDE_REDUCE  # the processor blocks' slabs are reduced already
         if defer and GRAD_READY is None and not defer_dense:
             join()
-            nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
+            if not side_reduced:
+                nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
         if overlap:
             for ev in done:
                 if ev is not None:
@@ -768,9 +784,10 @@ class EPDFunction(torch.autograd.Function):
                                   ctypes.pointer(dreds[2]), st)
                 join()
                 # ONE reduction for the whole model: decoder, every processor block, encoders
-                allr = (nat.WgradReduce * (3 + (2 * nb if defer else 0)))()
+                npr = 2 * nb if defer and not side_reduced else 0
+                allr = (nat.WgradReduce * (3 + npr))()
                 allr[0] = dreds[0]
-                for i in range(2 * nb if defer else 0):
+                for i in range(npr):
                     allr[1 + i] = reds[i]
                 allr[len(allr) - 2], allr[len(allr) - 1] = dreds[1], dreds[2]
                 nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
