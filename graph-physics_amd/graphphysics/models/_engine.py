@@ -104,6 +104,9 @@ CONC_WS = os.environ.get("MGN_CONC_WS", "2")
 # 344.1 -> 345.1 steps/s, sustained 352.3 -> 354.6: the end-of-backward reduction leaves the critical
 # path). MGN_SIDE_REDUCE=0: one reduction at the end
 SIDE_REDUCE = os.environ.get("MGN_SIDE_REDUCE", "1") == "1"
+# concurrent backward: the encoders' weight-gradient launches sized for the data share of the CUs
+# (MGN_ENC_CAP=0: the weight-gradient share, as the processor's rings)
+ENC_DATA_CAP = os.environ.get("MGN_ENC_CAP", "1") == "1"
 
 
 def conc_caps(E, chained):
@@ -748,6 +751,11 @@ class EPDFunction(torch.autograd.Function):
                 ev.record(side)
                 done[b % 2] = ev
             dx, de = dx1, de1
+        if conc and ENC_DATA_CAP:
+            # the encoders' backward runs beside block 0's ring launch: its weight-gradient launches take
+            # the data share of the chip too (capped at the ring's share they took 63 instead of ~40 us)
+            nat.check(L.mgn_set_grid_cus(caps[0], caps[0]))
+
         def join():  # the side stream's weight gradients are complete before their reduction
             if conc:
                 nat.check(L.mgn_set_grid_cus(0, 0))
