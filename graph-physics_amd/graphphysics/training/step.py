@@ -116,6 +116,16 @@ class TrainStep:
         n = getattr(ex, "mgn_skipped_updates", 0)
         if n:
             self._rewind(n)
+        if self.dp and self.world > 1:
+            # data parallelism: the device skipped the update on THIS rank only, the other
+            # ranks applied theirs, so the replicas no longer agree; as an exception on one rank of the
+            # reference's DDP job ends that job, every later step of this TrainStep refuses to run
+            self._dp_diverged = "%s: %s" % (type(ex).__name__, ex)
+
+    def _check_replicas(self):
+        if getattr(self, "_dp_diverged", None):
+            raise RuntimeError("data-parallel TrainStep after a validation error on this rank (%s): the "
+                               "replicas' parameters differ; restart from a checkpoint" % self._dp_diverged)
 
     def _rewind(self, n):
         for g in self.opt.param_groups:
@@ -142,6 +152,7 @@ class TrainStep:
         sc._last_lr = list(lrs)
 
     def eager(self):
+        self._check_replicas()
         try:
             nat.poll_errors(self.batch.x.device)
             self.opt.zero_grad(set_to_none=True)
@@ -315,6 +326,7 @@ class TrainStep:
     def __call__(self):
         if not self.use_graph:
             return self.eager()
+        self._check_replicas()
         dev = self.batch.x.device
         try:
             nat.poll_errors(dev)

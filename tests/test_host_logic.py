@@ -257,3 +257,25 @@ def test_padded_plan_layout_round_trips(h):
     assert enc.shapes[0][:2] == (W, 11) and enc.out_width == W
     with pytest.raises(ValueError, match="at most 128"):
         _engine.kernel_width(144)
+
+
+def test_data_parallel_step_refuses_to_continue_after_validation_error():
+    """under data parallelism a validation error skips the optimizer update on the raising
+    rank only, so the replicas diverge; the TrainStep then refuses further steps (as an exception on one
+    rank ends the reference's DDP job) instead of continuing silently. Single-process steps are unaffected."""
+    import pytest
+    from graphphysics.training.step import TrainStep
+
+    class _Opt:
+        param_groups = []
+        state = {}
+
+    for dp, world, refuses in ((True, 2, True), (True, 1, False), (False, 1, False)):
+        ts = TrainStep.__new__(TrainStep)
+        ts.dp, ts.world, ts.opt, ts.sched = dp, world, _Opt(), None
+        ts._raised(IndexError("edge_index out of range"))
+        if refuses:
+            with pytest.raises(RuntimeError, match="replicas"):
+                ts._check_replicas()
+        else:
+            ts._check_replicas()

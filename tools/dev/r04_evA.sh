@@ -1,0 +1,8 @@
+#!/bin/bash
+# final evidence, part A: GPU suite, smoke, rocprofv3 + PMC of bf16 Cfg B and fp32 Cfg B
+TAG=${1:-r04c}
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?; echo tests=$rc; tail -1 gpurun_out/gpu_tests_$TAG.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit 1
+echo smoke=ok
+bash tools/profile_round.sh $TAG && bash tools/profile_round.sh ${TAG}f --dtype fp32
