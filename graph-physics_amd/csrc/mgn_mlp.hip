@@ -3506,10 +3506,13 @@ static size_t mlp_keep_bytes(const mgn_mlp* m, int64_t rows) {
            align_up((size_t)wgrad_max_chunks(rows_pad(rows), m->hidden) * grad_G(m) * sizeof(float));
 }
 
+// part: 0 = data + weight gradients; MGN_BWD_DATA_ONLY = the data gradients (and the saves the weight
+// gradients read; defer->ntiles = the dscale partial rows written); MGN_BWD_WGRAD_ONLY = the weight
+// gradients of an earlier DATA_ONLY call over the same buffers (defer->ntiles as it left it)
 static int mlp_backward_entry(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld, const int32_t* in_rows,
                               int64_t rows, const mgn_mlp_saved* saved, const void* dout, int32_t dout_dtype, void* din,
                               int32_t din_dtype, float* grads, void* ws, size_t ws_bytes, void* keep, RedDesc* defer,
-                              hipStream_t st) {
+                              hipStream_t st, int32_t part = 0) {
     if (int e = check_mlp(m)) return e;
     MGN_REQUIRE(ws_bytes >= mlp_bwd_ws(m, rows), "backward workspace too small");
     const bool chained = chain_dense_eligible(m) && rows > 0;
@@ -3521,12 +3524,16 @@ static int mlp_backward_entry(const mgn_mlp* m, const void* in, int32_t in_dtype
     char* q = keep ? reinterpret_cast<char*>(keep) : p;
     float* dsp = reinterpret_cast<float*>(q);
     q += align_up((size_t)(keep ? rows_pad(rows) / 16 : ntiles) * m->out_dim * sizeof(float));
-    float* part = reinterpret_cast<float*>(q);
+    float* part_buf = reinterpret_cast<float*>(q);
     if (rows == 0) {
-        MGN_TRY(hipMemsetAsync(grads, 0, (grad_G(m) + (m->has_norm ? m->out_dim : 0)) * sizeof(float), st));
+        if (part != MGN_BWD_DATA_ONLY)
+            MGN_TRY(hipMemsetAsync(grads, 0, (grad_G(m) + (m->has_norm ? m->out_dim : 0)) * sizeof(float), st));
         return 0;
     }
-    if (chained) {
+    if (part == MGN_BWD_WGRAD_ONLY) {
+        MGN_REQUIRE(defer && defer->ntiles > 0, "MGN_BWD_WGRAD_ONLY needs the reduce descriptor of the DATA_ONLY call");
+        ntiles = defer->ntiles;
+    } else if (chained) {
         // chained data gradients (dZ of every layer, din) + the generic weight gradients over the
         // same R8 operands
         MGN_REQUIRE(dout_dtype == MGN_F32 || dout_dtype == MGN_BF16, "dout dtype must be MGN_F32 or MGN_BF16");
@@ -3542,11 +3549,16 @@ static int mlp_backward_entry(const mgn_mlp* m, const void* in, int32_t in_dtype
         o.din_ld = m->in_dim;
         if (int e = mlp_bwd_any(m, MODE_DENSE, rows, saved, dout, dout_dtype, m->out_dim, o, dz, dsp, st)) return e;
     }
+    if (part == MGN_BWD_DATA_ONLY) {
+        memset(defer, 0, sizeof(*defer));
+        defer->ntiles = ntiles;  // blocks = 0: nothing to reduce yet
+        return 0;
+    }
     int nchunks = 0;
-    if (int e = mlp_wgrad_any(m, rows, saved->act, dz, dsp, ntiles, part, grads, nullptr, 0, &nchunks, defer == nullptr,
-                              st))
+    if (int e = mlp_wgrad_any(m, rows, saved->act, dz, dsp, ntiles, part_buf, grads, nullptr, 0, &nchunks,
+                              defer == nullptr, st))
         return e;
-    if (defer) *defer = red_desc(m, part, nchunks, dsp, ntiles, grads);
+    if (defer) *defer = red_desc(m, part_buf, nchunks, dsp, ntiles, grads);
     return 0;
 }
 
@@ -3568,14 +3580,29 @@ int mgn_mlp_backward_deferred(const mgn_mlp* m, const void* in, int32_t in_dtype
                               int32_t dout_dtype, void* din, int32_t din_dtype, float* grads, void* ws,
                               size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce1,
                               mgn_stream_t stream) {
+    return mgn_mlp_backward_deferred2(m, in, in_dtype, in_ld, in_rows, rows, saved, dout, dout_dtype, din, din_dtype,
+                                      grads, ws, ws_bytes, keep, keep_bytes, reduce1, 0, stream);
+}
+
+int mgn_mlp_backward_deferred2(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                               const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved, const void* dout,
+                               int32_t dout_dtype, void* din, int32_t din_dtype, float* grads, void* ws,
+                               size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce1,
+                               int32_t flags, mgn_stream_t stream) {
     MGN_REQUIRE(reduce1 && keep, "keep buffer and reduce1 required");
-    memset(reduce1, 0, sizeof(mgn_wgrad_reduce));
+    const int32_t part = flags & (MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY);
+    MGN_REQUIRE(!(flags & ~(MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY)) && part != (MGN_BWD_DATA_ONLY | MGN_BWD_WGRAD_ONLY),
+                "flags: 0, MGN_BWD_DATA_ONLY or MGN_BWD_WGRAD_ONLY");
     if (int e = check_mlp(m)) return e;
     MGN_REQUIRE(keep_bytes >= mlp_keep_bytes(m, rows), "mlp backward keep buffer too small");
     RedDesc d;
-    memset(&d, 0, sizeof(d));
+    if (part == MGN_BWD_WGRAD_ONLY)
+        memcpy(&d, reduce1, sizeof(d));  // the DATA_ONLY call's partial-row count
+    else
+        memset(&d, 0, sizeof(d));
+    memset(reduce1, 0, sizeof(mgn_wgrad_reduce));
     if (int e = mlp_backward_entry(m, in, in_dtype, in_ld, in_rows, rows, saved, dout, dout_dtype, din, din_dtype, grads,
-                                   ws, ws_bytes, keep, &d, (hipStream_t)stream))
+                                   ws, ws_bytes, keep, &d, (hipStream_t)stream, part))
         return e;
     memcpy(reduce1, &d, sizeof(d));
     return 0;

@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 13  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 14  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -84,6 +84,9 @@ EXPORTS = {
     "mgn_mlp_backward_deferred": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
                                          ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp, _sz,
                                          ctypes.POINTER(WgradReduce), _vp]),
+    "mgn_mlp_backward_deferred2": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
+                                          ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp, _sz,
+                                          ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_block_forward_inference_supported": (_i32, [ctypes.POINTER(Mlp), ctypes.POINTER(Mlp)]),
     "mgn_block_forward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
                                                 ctypes.POINTER(Mlp)]),

@@ -107,6 +107,9 @@ SIDE_REDUCE = os.environ.get("MGN_SIDE_REDUCE", "1") == "1"
 # concurrent backward: the encoders' weight-gradient launches sized for the data share of the CUs
 # (MGN_ENC_CAP=0: the weight-gradient share, as the processor's rings)
 ENC_DATA_CAP = os.environ.get("MGN_ENC_CAP", "1") == "1"
+# concurrent backward: the decoder's weight gradients on the side stream beside the last block's data
+# half (MGN_DEC_SPLIT=0: right after its data gradients on the current stream)
+DEC_SPLIT = os.environ.get("MGN_DEC_SPLIT", "1") == "1"
 
 
 def conc_caps(E, chained):
@@ -480,6 +483,16 @@ def _mlp_bwd_deferred(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dou
         keep.numel(), red, stream))
 
 
+def _mlp_bwd_half(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws, keep,
+                  red, flags, stream):
+    """One half of _mlp_bwd_deferred (mgn_mlp_backward_deferred2, ABI v14): flags MGN_BWD_DATA_ONLY, then
+    MGN_BWD_WGRAD_ONLY with the same arguments (red carries the partial-row count between them)."""
+    nat.check(nat.lib().mgn_mlp_backward_deferred2(
+        ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld, nat.ptr(rows_idx), rows, ctypes.byref(saved),
+        nat.ptr(dout), dout_mdt, nat.ptr(din), din_mdt, nat.ptr(grads), nat.ptr(ws), ws.numel(), nat.ptr(keep),
+        keep.numel(), red, flags, stream))
+
+
 def _mlp_keep(desc, rows, dev):
     n = int(nat.lib().mgn_mlp_backward_keep_bytes(ctypes.byref(desc), rows))
     return torch.empty(max(n, 256), dtype=torch.uint8, device=dev)
@@ -633,8 +646,15 @@ class EPDFunction(torch.autograd.Function):
             dx = torch.empty((N, H), dtype=tdt, device=dev)
             g = _padc(gout.detach().float(), plan.specs[2].out_width).contiguous()
             if defer_dense:
-                _mlp_bwd_deferred(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
-                                  ctypes.c_void_p(gp + 4 * off[2]), ws, keeps[0], ctypes.pointer(dreds[0]), st)
+                # the decoder's data gradients now, its weight gradients once the processor's schedule is
+                # known (beside the last block's data half on the concurrent backward); own workspace
+                wsd = torch.empty(max(_ws_bytes_mlp(descs[2], N), 1), dtype=torch.uint8, device=dev)
+                dec_args = (descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
+                            ctypes.c_void_p(gp + 4 * off[2]), wsd, keeps[0], ctypes.pointer(dreds[0]))
+                _mlp_bwd_half(*dec_args, nat.MGN_BWD_DATA_ONLY, st)
+                if not DEC_SPLIT:  # weight gradients at once, on the whole chip
+                    _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, st)
+                    dec_args = None
             else:
                 _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                          ctypes.c_void_p(gp + 4 * off[2]), ws, st)
@@ -685,6 +705,12 @@ class EPDFunction(torch.autograd.Function):
             wss = [torch.empty_like(ws) for _ in range(nws)]
             done = [None] * nws
             nat.check(L.mgn_set_grid_cus(*caps))
+        if defer_dense and dec_args is not None:  # the decoder's weight gradients (concurrent backward: on
+            if conc:                                  # the side stream, beside block nb-1's data half)
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+            _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, nat._vp(side.cuda_stream) if conc else st)
         for b in reversed(range(nb)):
             dx1 = torch.empty((N, H), dtype=tdt, device=dev)
             de1 = torch.empty((E, H), dtype=tdt, device=dev)

@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 13
+#define MGN_ABI_VERSION 14
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -266,6 +266,17 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
                                  void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
                                  int32_t flags, mgn_stream_t stream);
 int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream);
+/* ABI v14: mgn_mlp_backward_deferred in two halves over the same arguments (flags 0 = the whole call):
+ * MGN_BWD_DATA_ONLY runs the data gradients (din, and the dZ saves / partials the weight gradients read
+ * in `ws` / `keep`) and leaves in reduce1 only the partial-row count; MGN_BWD_WGRAD_ONLY, given that
+ * reduce1, runs the weight gradients (on another stream if the caller orders it after DATA_ONLY) and
+ * fills reduce1 for mgn_wgrad_reduce_many. EncodeProcessDecode's decoder (reference processors.py:131)
+ * uses it to run its weight gradients beside the first processor block's data gradients. */
+int mgn_mlp_backward_deferred2(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                               const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved,
+                               const void* dout, int32_t dout_dtype, void* din, int32_t din_dtype,
+                               float* grads, void* ws, size_t ws_bytes, void* keep, size_t keep_bytes,
+                               mgn_wgrad_reduce* reduce1, int32_t flags, mgn_stream_t stream);
 /* ABI v13: caps on the CUs the persistent grids of later launches are sized for (0 = the whole
  * device): data_cus for every launch except the weight-gradient launches, wgrad_cus for those. Host
  * state of the library, read when a launch is issued (a captured hipGraph keeps the grids it

@@ -90,7 +90,7 @@ int main(void) {
 def test_host_size_functions(lib):
     from graphphysics import _native as nat
 
-    assert lib.mgn_abi_version() == 13
+    assert lib.mgn_abi_version() == 14
     # fragment-packed Linear: max(fwd, transposed) fragment count x 64 lanes x VEC
     assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_BF16) == max(8 * 12, 24 * 4) * 64 * 8
     assert lib.mgn_linear_pack_elems(2, 128, nat.MGN_F32) == max(1 * 32, 8 * 1) * 64
