@@ -118,7 +118,10 @@ def conc_caps(E, chained):
     16-row tiles per wave on the whole chip (Cfg B: 1.8) — with the chip split 160 + 96 (measured,
     Cfg B bf16: 332 -> 342 steps/s; 192 + 64: 297, 128 + 128: 322, both uncapped: 317). Measured
     slower, so one stream: fp32 Cfg B (its MFMA-bound ring: 98 -> 87), Cfg C at plate.json's sizes
-    (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5 -> 32.7); Cfg A neutral."""
+    (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5 -> 32.7). The small graphs
+    lose to the cross-stream dependencies of the replayed graph even with one workspace per block (no
+    wait on the main stream): Cfg A 1720 -> 1515 uncapped / 1420 at 160 + 96, Cfg C 1034 -> 870 / 883
+    (profiles/r04_ab.txt, r04_ab8.sh)."""
     v = CONC_WGRAD
     if v == "0":
         return None
