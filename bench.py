@@ -292,19 +292,15 @@ def analyse(a, prof, sim, lay, N, E, dt):
                       + 2 * (lay["node_in"] * h + 3 * h * h) * N + 2 * (3 * h * h + h * lay["out"]) * N)
     step_tf = step_flops * a.steps / dt / 1e12
     if kinds:
-        # dominant kernel class = largest device time per step in the REPLAYED graph (rocprofv3 kernel
-        # trace of this bench command on these sources, recorded with the PMC passes under profiles/);
-        # without such a record, the largest class of the eager HIP-event profile
+        # dominant kernel class = largest device time per step of the one-stream per-class profile (each
+        # kernel on the whole chip, the launches avg_launch_us times); its share of the
+        # REPLAYED step (rocprofv3 kernel trace of this bench command on these sources, recorded with the PMC
+        # passes under profiles/, where the ring shares the chip with the data gradients) beside it
+        dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
+        picked = "one-stream per-class profile (%s)" % ", ".join(
+            "%s %.1f us/step" % (k, 1000 * kinds[k]["ms_per_step"])
+            for k in sorted(kinds, key=lambda k: -kinds[k]["total_ms"])[:3])
         rep = replay_lookup(wl)
-        cands = [k for k in rep.get("replay", {}) if k in kinds]
-        if cands:
-            dom = max(cands, key=lambda k: rep["replay"][k]["us_per_step"])
-            picked = "replay: %s (%s)" % (rep["source"], ", ".join(
-                "%s %.1f us/step" % (k, rep["replay"][k]["us_per_step"])
-                for k in sorted(cands, key=lambda k: -rep["replay"][k]["us_per_step"])[:3]))
-        else:
-            dom = max(kinds, key=lambda k: kinds[k]["total_ms"])
-            picked = "eager HIP-event profile (no replay trace recorded for these sources and workload)"
         kd = kinds[dom]
         bound, executed, algorithmic = work.get(dom, ("mfma", 0, None))
         credit = algorithmic if algorithmic is not None else executed
@@ -316,6 +312,14 @@ def analyse(a, prof, sim, lay, N, E, dt):
         peak = PEAK[a.dtype] if bound == "mfma" else HBM_PEAK
         pmc = pmc_lookup(dom, wl)
         unit = "flops" if bound == "mfma" else "bytes"
+        in_replay = None
+        rr = rep.get("replay", {}).get(dom)
+        if rr and rr.get("avg_us"):
+            in_replay = {"source": rep["source"], "us_per_step": rr["us_per_step"], "avg_us": rr["avg_us"],
+                         "launches_per_step": rr["launches_per_step"],
+                         "frac": round(per_launch / (rr["avg_us"] * 1e-6) / scale / peak, 4),
+                         "note": "the same work per launch over the class's average launch in the replayed step "
+                                 "(concurrent schedule: the ring on its share of the CUs)"}
         roof = {"kernel": dom, "bound": bound, "achieved": round(ach, 2), "peak": peak,
                 "unit": "TFLOP/s" if bound == "mfma" else "GB/s", "frac": round(ach / peak, 4),
                 "credit": "algorithmic (SURVEY §8(d): the reference algorithm's work this kernel class stands for)"
@@ -324,11 +328,17 @@ def analyse(a, prof, sim, lay, N, E, dt):
                              "frac": round(ach_x / peak, 4)},
                 "traffic": pmc.get("hbm_bytes"), "traffic_source": pmc.get("source"),
                 "mfma_util_measured": pmc.get("mfma_util"), "dominant_from": picked,
+                "in_replay_frac": in_replay["frac"] if in_replay else None, "in_replay": in_replay,
+                "pmc_record": {k: pmc.get(k) for k in ("schedule", "trace_us", "grbm_us_at_2400MHz",
+                                                       "implied_clock_mhz", "instances")},
                 unit + "_per_launch": per_launch,
                 "avg_launch_us": round(avg_s * 1e6, 2), "launches_per_step": kd["launches"] / a.steps,
                 "peak_source": "MI355X_MICROARCH.md: dense bf16 MFMA 2.5 PFLOP/s (fp32 MFMA 157.3), HBM3E 8 TB/s",
                 "step": {"tflops_per_s": round(step_tf, 2), "frac": round(step_tf / PEAK[a.dtype], 4),
                          "flops_per_step": step_flops, "note": "3 x F_fwd (SURVEY §8d) / measured ms_per_step"}}
+        if pmc.get("trace_us"):
+            # the PMC record's own launches (rocprofv3 trace of the one-stream run) vs this run's HIP events
+            roof["pmc_record"]["trace_us_over_avg_launch_us"] = round(pmc["trace_us"] / (avg_s * 1e6), 3)
         if "fwd_node" in kinds:  # the segmented sum is fused into the node-MLP forward (CSC segments)
             sb = scatter_bytes(N, E, h, es)
             t = kinds["fwd_node"]["total_ms"] / 1000 / kinds["fwd_node"]["launches"]
@@ -431,6 +441,7 @@ def main():
         for k, v in base.items():
             setattr(data, k, v.clone())
 
+    ctl0 = step.ctl_seconds
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if a.fresh_batch:
@@ -440,6 +451,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ctl_ms = 1000 * (step.ctl_seconds - ctl0) / a.steps  # host gloo re-capture agreement (N > 1, graph mode)
     log("timed steps done: %.3f ms/step" % (1000 * dt / a.steps))
     # sustained rate: the same step replayed for about `sustain` more seconds (reported beside the
     # headline, never as `value`; it also keeps the GPU visibly busy for the driver's sampler)
@@ -484,6 +496,9 @@ def main():
                    "stats_allreduce_bytes_per_step": 4 * stats.numel() if stats is not None else None,
                    "grad_buckets_cover_all_params": covered == nparams if covered >= 0 else None,
                    "grad_buckets_per_step": step.buckets.issued if (step.overlap and step.buckets) else None,
+                   "recapture_agreement_ms_per_step": round(ctl_ms, 4),
+                   "recapture_agreement": "host gloo MAX all-reduce of one int per step (TrainStep._ctl), inside "
+                                          "the timed region",
                    "backend": dist.get_backend()}
     last_loss = float(loss.item())
 
@@ -581,7 +596,9 @@ def replay_lookup(workload):
 def pmc_lookup(kernel_class, workload):
     """PMC figures of `kernel_class` from the newest committed profiles/*_traffic.json measured on the
     same kernel sources (sha256 stamp) AND the same workload, averaged over that class's kernel
-    instances weighted by their launches (the class time bench.py reports averages the same launches)."""
+    instances weighted by their launches (the class time bench.py reports averages the same launches).
+    Only records whose PMC passes ran on one stream (tools/profile_round.sh: MGN_CONC_WGRAD=0), the
+    schedule of bench.py's per-class timing."""
     import glob
 
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -592,12 +609,16 @@ def pmc_lookup(kernel_class, workload):
         d = json.load(open(f))
         if d.get("sources_sha") != sha or d.get("workload") != workload:
             continue
+        if not d.get("schedule", "").startswith("one stream"):
+            continue  # a record of the concurrent schedule describes other launches than avg_launch_us times
         inst = [v for v in d.get("kernels", {}).values() if v.get("class") == kernel_class]
-        out = {"source": os.path.relpath(f, ROOT), "instances": [v["kernel"][:80] for v in inst]}
-        for field in ("hbm_bytes", "mfma_util"):
+        out = {"source": os.path.relpath(f, ROOT), "instances": [v["kernel"][:80] + " grid=" + v["grid"] for v in inst],
+               "schedule": d.get("schedule", "default (MGN_CONC_WGRAD=auto)")}
+        for field in ("hbm_bytes", "mfma_util", "trace_us", "grbm_us_at_2400MHz", "implied_clock_mhz"):
             vals = [(v[field], v.get("launches", 1)) for v in inst if field in v]
             if vals:
-                out[field] = round(sum(x * w for x, w in vals) / sum(w for _, w in vals), 4 if field == "mfma_util" else 0)
+                out[field] = round(sum(x * w for x, w in vals) / sum(w for _, w in vals), 4 if field == "mfma_util" else 0
+                                   if field == "hbm_bytes" else 2)
         return out
     return {"source": "no PMC pass on these kernel sources and workload (run tools/profile_round.sh)"}
 

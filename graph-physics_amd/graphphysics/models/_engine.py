@@ -112,25 +112,46 @@ ENC_DATA_CAP = os.environ.get("MGN_ENC_CAP", "1") == "1"
 DEC_SPLIT = os.environ.get("MGN_DEC_SPLIT", "1") == "1"
 
 
-def conc_caps(E, chained):
+def conc_caps(E, chained, dev=None):
     """(data CUs, weight-gradient CUs) of the concurrent backward, or None (one stream). "auto": only
     the chained bf16 h=128 blocks in the latency-bound regime — their persistent edge kernels run 1-4
-    16-row tiles per wave on the whole chip (Cfg B: 1.8) — with the chip split 160 + 96 (measured,
-    Cfg B bf16: 332 -> 342 steps/s; 192 + 64: 297, 128 + 128: 322, both uncapped: 317). Measured
-    slower, so one stream: fp32 Cfg B (its MFMA-bound ring: 98 -> 87), Cfg C at plate.json's sizes
-    (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5 -> 32.7). The small graphs
-    lose to the cross-stream dependencies of the replayed graph even with one workspace per block (no
-    wait on the main stream): Cfg A 1720 -> 1515 uncapped / 1420 at 160 + 96, Cfg C 1034 -> 870 / 883
-    (profiles/r04_ab.txt, r04_ab8.sh)."""
+    16-row tiles per wave on the whole chip (Cfg B: 1.8) — with the chip split 5/8 + 3/8 (MI355X's 256
+    CUs: 160 + 96; measured, Cfg B bf16: 332 -> 342 steps/s; 192 + 64: 297, 128 + 128: 322, both
+    uncapped: 317). The CU count is the device's (a partitioned device or another SKU scales the split
+    and the regime estimate). Measured slower, so one stream: fp32 Cfg B (its MFMA-bound ring: 98 ->
+    87), Cfg C at plate.json's sizes (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5
+    -> 32.7). The small graphs lose to the cross-stream dependencies of the replayed graph even with one
+    workspace per block (no wait on the main stream): Cfg A 1720 -> 1515 uncapped / 1420 at 160 + 96,
+    Cfg C 1034 -> 870 / 883 (profiles/r04_ab.txt, r04_ab8.sh)."""
     v = CONC_WGRAD
     if v == "0":
         return None
     if v != "auto":
         d, r = (int(t) for t in v.split(","))
         return d, r
-    tiles_per_wave = E / (16 * 12 * 256)
-    return (160, 96) if chained and 1.0 <= tiles_per_wave <= 4.0 else None
+    cus = _device_cus(dev)
+    tiles_per_wave = E / (16 * 12 * cus)
+    if not (chained and 1.0 <= tiles_per_wave <= 4.0):
+        return None
+    d = (cus * 5 + 4) // 8
+    return d, cus - d
+
+
+_CUS = {}
+
+
+def _device_cus(dev):
+    """Compute units of the device (MI355X: 256)."""
+    dev = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+    n = _CUS.get(dev.index)
+    if n is None:
+        n = _CUS[dev.index] = int(torch.cuda.get_device_properties(dev).multi_processor_count)
+    return n
+
+
 _SIDE = {}
+# the schedule the last EncodeProcessDecode backward ran (tests assert which path a step took)
+LAST_SCHEDULE = {}
 # Inspection hook (tests: mask-pinned parity): INSPECT(dict) is called at the end of every training
 # forward of EncodeProcessDecode with the forward saves (topology, plan, per-MLP saved buffers), so a
 # check can read the ReLU branch each hidden unit took. None: no call.
@@ -621,6 +642,7 @@ class EPDFunction(torch.autograd.Function):
         tdt = nat.torch_dtype(mdt)
         N, E, H = topo.num_nodes, topo.num_edges, ctx.H
         descs = pw.descs
+        L = nat.lib()
         # the kernels write gradients in the (zero-)padded parameter layout; a plan of kernel-width
         # MLPs has the true layout (offsets_pad == offsets, no gather at the end)
         G = torch.empty(plan.numel_pad, dtype=torch.float32, device=dev)
@@ -632,17 +654,55 @@ class EPDFunction(torch.autograd.Function):
             bdescs, boff = descs, off
         else:
             bdescs, boff = descs[3:], off[3:]
+        nb = len(bdescs) // 2
+        chained = nb > 0 and all(
+            L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
+            for b in range(nb))
+        # Each block: the data half (dx, de) on the current stream; the weight-gradient half on a side
+        # stream, overlapped with the next block's data half (two workspaces alternate; a workspace is
+        # reused only after the side stream has finished with it). Joined before returning.
+        overlap = OVERLAP_WGRAD and nb > 1
+        # deferred weight-gradient reductions: each block leaves its slabs in its own keep buffer and
+        # ONE launch reduces them all after the last block; with a gradient-ready callback (the
+        # data-parallel bucketed all-reduce) one launch per group of blocks whose gradients fill a
+        # bucket (GRAD_GROUP_BYTES), handed over as one range as soon as the group's backward ends
+        defer = DEFER_REDUCE and not overlap and nb > 0
+        # concurrent backward (weight-gradient launches beside the next block's data gradients), with or
+        # without a gradient-ready callback: under data parallelism each block's slabs are reduced on the
+        # side stream right after its ring and the range is handed over THERE, so the bucketed all-reduce
+        # waits for the side stream's work, not for the main stream (GradBuckets records per stream)
+        caps = conc_caps(E, chained, dev)
+        conc = caps is not None and defer and nb > 1
+        side_reduced = conc and (SIDE_REDUCE or GRAD_READY is not None)
+        # encoders' and decoder's reductions deferred into the final mgn_wgrad_reduce_many too (one
+        # reduction launch per backward). With a gradient-ready callback only on the concurrent
+        # backward, where the decoder is reduced and handed over right after its weight gradients
+        # (early_dec) and the encoders, last anyway, in the final launch
+        defer_dense = DEFER_REDUCE and not ctx.only_processor and not OVERLAP_WGRAD and (GRAD_READY is None or conc)
+        early_dec = defer_dense and GRAD_READY is not None
+        LAST_SCHEDULE.update(conc=caps if conc else None, side_reduced=side_reduced, defer_dense=defer_dense,
+                             early_dec=early_dec, grad_ready=GRAD_READY is not None)
         need = _ws_bytes_block(topo, bdescs[0], bdescs[1]) if len(bdescs) >= 2 else 0
         if not ctx.only_processor:
             need = max(need, _ws_bytes_mlp(descs[0], N), _ws_bytes_mlp(descs[1], E),
                        _ws_bytes_mlp(descs[2], N))
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-        # encoders' and decoder's reductions deferred into the final mgn_wgrad_reduce_many too (one
-        # reduction launch per backward); not with a gradient-ready callback (its ranges hand over early)
-        defer_dense = DEFER_REDUCE and not ctx.only_processor and GRAD_READY is None and not OVERLAP_WGRAD
         if defer_dense:
             dreds = (nat.WgradReduce * 3)()  # decoder, node encoder, edge encoder
             keeps = [_mlp_keep(descs[2], N, dev), _mlp_keep(descs[0], N, dev), _mlp_keep(descs[1], E, dev)]
+        main = torch.cuda.current_stream(dev)
+        side = _side_stream(dev) if (conc or overlap) else None
+        dec_args = None
+
+        def dec_wgrad(stream):
+            """The decoder's weight-gradient half on `stream` (early_dec: reduced and handed over there)."""
+            sp = nat._vp(stream.cuda_stream)
+            _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, sp)
+            if early_dec:
+                nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(dreds[0]), 1, sp))
+                with torch.cuda.stream(stream):
+                    ready(G, off[2], off[2] + plan.specs[2].numel)
+
         if ctx.only_processor:
             dx = _padc(gout.detach(), H).to(tdt).contiguous()
         else:
@@ -655,35 +715,22 @@ class EPDFunction(torch.autograd.Function):
                 dec_args = (descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                             ctypes.c_void_p(gp + 4 * off[2]), wsd, keeps[0], ctypes.pointer(dreds[0]))
                 _mlp_bwd_half(*dec_args, nat.MGN_BWD_DATA_ONLY, st)
-                if not DEC_SPLIT:  # weight gradients at once, on the whole chip
-                    _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, st)
+                if not (DEC_SPLIT and conc):  # weight gradients at once, on the whole chip
+                    dec_wgrad(main)
                     dec_args = None
             else:
                 _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                          ctypes.c_void_p(gp + 4 * off[2]), ws, st)
-            ready(G, off[2], off[2] + plan.specs[2].numel)
-        nb = len(bdescs) // 2
+                ready(G, off[2], off[2] + plan.specs[2].numel)
         # the last block's e' is discarded (EncodeProcessDecode returns nodes): its edge-output
         # gradient is zero, which the chained bf16 kernels take as NULL (no zero fill, no reads)
         de = None if nb and nat.lib().mgn_block_forward_inference_supported(
             ctypes.byref(bdescs[2 * nb - 2]), ctypes.byref(bdescs[2 * nb - 1])) else \
             torch.zeros((E, H), dtype=tdt, device=dev)
-        L = nat.lib()
-        # Each block: the data half (dx, de) on the current stream; the weight-gradient half on a side
-        # stream, overlapped with the next block's data half (two workspaces alternate; a workspace is
-        # reused only after the side stream has finished with it). Joined before returning.
-        overlap = OVERLAP_WGRAD and nb > 1
-        # deferred weight-gradient reductions: each block leaves its slabs in its own keep buffer and
-        # ONE launch reduces them all after the last block; with a gradient-ready callback (the
-        # data-parallel bucketed all-reduce) one launch per group of blocks whose gradients fill a
-        # bucket (GRAD_GROUP_BYTES), handed over as one range as soon as the group's backward ends
-        defer = DEFER_REDUCE and not overlap and nb > 0
         pend_hi = pend_b = None  # open group: the range end of its first (highest) block, that block
         # every block on the chained bf16 h=128 kernels (the pair-layout de needs them on both sides;
         # a graph without edges or nodes runs the generic kernels: row-major)
-        pair_de = PAIR_DE and not overlap and de is None and N > 0 and E > 0 and all(
-            L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
-            for b in range(nb))
+        pair_de = PAIR_DE and not overlap and de is None and N > 0 and E > 0 and chained
         if defer:
             kb = max(int(L.mgn_block_backward_keep_bytes(ctypes.byref(topo.struct), ctypes.byref(bdescs[0]),
                                                          ctypes.byref(bdescs[1]))), 256)
@@ -691,152 +738,155 @@ class EPDFunction(torch.autograd.Function):
             keep = torch.empty(nb * kb, dtype=torch.uint8, device=dev)
             reds = (nat.WgradReduce * (2 * nb))()
         if overlap:
-            main = torch.cuda.current_stream(dev)
-            side = _side_stream(dev)
             wss = [ws, torch.empty_like(ws)]
             done = [None, None]
-        # weight-gradient launches beside the next block's data gradients (the encoders' backward
-        # reuses ws only after the side stream is done with block 1's workspace)
-        caps = conc_caps(E, nb > 0 and all(
-            L.mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
-            for b in range(nb)))
-        conc = caps is not None and defer and GRAD_READY is None and nb > 1
         if conc:
-            main = torch.cuda.current_stream(dev)
-            side = _side_stream(dev)
             nws = nb if CONC_WS == "all" else max(int(CONC_WS), 2)
             wss = [torch.empty_like(ws) for _ in range(nws)]
             done = [None] * nws
+            # process-global CU caps of libmgn's launches: reset in the finally below, so an error
+            # anywhere in the concurrent section never leaves later launches capped
             nat.check(L.mgn_set_grid_cus(*caps))
-        if defer_dense and dec_args is not None:  # the decoder's weight gradients (concurrent backward: on
-            if conc:                                  # the side stream, beside block nb-1's data half)
-                ev = torch.cuda.Event()
+        try:
+            if dec_args is not None:  # the decoder's weight gradients on the side stream, beside block nb-1's
+                ev = torch.cuda.Event()  # data half
                 ev.record(main)
                 side.wait_event(ev)
-            _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, nat._vp(side.cuda_stream) if conc else st)
-        for b in reversed(range(nb)):
-            dx1 = torch.empty((N, H), dtype=tdt, device=dev)
-            de1 = torch.empty((E, H), dtype=tdt, device=dev)
-            args = (ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
-                    nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
-                    nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
-                    ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
-            # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
-            # layout); the first block's stay row-major (the encoders / the caller read them)
-            flags = 0
-            if pair_de:
-                if b + 1 < nb:
-                    flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
-                if b > 0:
-                    flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
-            if conc:
-                w = wss[b % nws]
-                if done[b % nws] is not None:
-                    main.wait_event(done[b % nws])  # the side stream is done reading this workspace
-                kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
-                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
-                                                         flags | nat.MGN_BWD_DATA_ONLY, st))
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
-                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb, ctypes.pointer(reds[2 * b]),
-                                                         flags | nat.MGN_BWD_WGRAD_ONLY, nat._vp(side.cuda_stream)))
-                if SIDE_REDUCE:
-                    nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2, nat._vp(side.cuda_stream)))
-                ev = torch.cuda.Event()
-                ev.record(side)
-                done[b % nws] = ev
-            elif defer:
-                nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
-                                                         ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
-                                                         ctypes.pointer(reds[2 * b]), flags, st))
-                if GRAD_READY is not None:
-                    if pend_hi is None:
-                        pend_b = b
-                        pend_hi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
-                    if (pend_hi - boff[2 * b]) * 4 >= GRAD_GROUP_BYTES or b == 0:
-                        # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
-                        nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1), st))
-                        ready(G, boff[2 * b], pend_hi)
-                        pend_hi = pend_b = None
-            elif not overlap:
-                if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
-                    red2 = (nat.WgradReduce * 2)()
-                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(), None, 0, red2, flags,
-                                                             st))
+                dec_wgrad(side)
+            for b in reversed(range(nb)):
+                dx1 = torch.empty((N, H), dtype=tdt, device=dev)
+                de1 = torch.empty((E, H), dtype=tdt, device=dev)
+                args = (ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
+                        nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
+                        nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
+                        ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
+                blo = boff[2 * b]
+                bhi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
+                # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
+                # layout); the first block's stay row-major (the encoders / the caller read them)
+                flags = 0
+                if pair_de:
+                    if b + 1 < nb:
+                        flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
+                    if b > 0:
+                        flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
+                if conc:
+                    w = wss[b % nws]
+                    if done[b % nws] is not None:
+                        main.wait_event(done[b % nws])  # the side stream is done reading this workspace
+                    kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
+                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb,
+                                                             ctypes.pointer(reds[2 * b]),
+                                                             flags | nat.MGN_BWD_DATA_ONLY, st))
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    side.wait_event(ev)
+                    sp = nat._vp(side.cuda_stream)
+                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb,
+                                                             ctypes.pointer(reds[2 * b]),
+                                                             flags | nat.MGN_BWD_WGRAD_ONLY, sp))
+                    if side_reduced:
+                        nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2, sp))
+                        if GRAD_READY is not None:  # final on the side stream: the bucket waits there
+                            with torch.cuda.stream(side):
+                                ready(G, blo, bhi)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    done[b % nws] = ev
+                elif defer:
+                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
+                                                             ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
+                                                             ctypes.pointer(reds[2 * b]), flags, st))
+                    if GRAD_READY is not None:
+                        if pend_hi is None:
+                            pend_b, pend_hi = b, bhi
+                        if (pend_hi - blo) * 4 >= GRAD_GROUP_BYTES or b == 0:
+                            # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
+                            nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1),
+                                                              st))
+                            ready(G, blo, pend_hi)
+                            pend_hi = pend_b = None
+                elif not overlap:
+                    if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
+                        red2 = (nat.WgradReduce * 2)()
+                        nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(), None, 0, red2,
+                                                                 flags, st))
+                    else:
+                        nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
+                    ready(G, blo, bhi)
                 else:
-                    nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
-                ready(G, boff[2 * b], boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1))
-            else:
-                w = wss[b % 2]
-                if done[b % 2] is not None:
-                    main.wait_event(done[b % 2])  # the side stream is done reading this workspace
-                nat.check(L.mgn_block_backward_data(*args, nat.ptr(w), w.numel(), st))
-                ready = torch.cuda.Event()
-                ready.record(main)
-                side.wait_event(ready)
-                nat.check(L.mgn_block_backward_wgrad(*args, nat.ptr(w), w.numel(), nat._vp(side.cuda_stream)))
-                ev = torch.cuda.Event()
-                ev.record(side)
-                done[b % 2] = ev
-            dx, de = dx1, de1
-        if conc and ENC_DATA_CAP:
-            # the encoders' backward runs beside block 0's ring launch: its weight-gradient launches take
-            # the data share of the chip too (capped at the ring's share they took 63 instead of ~40 us)
-            nat.check(L.mgn_set_grid_cus(caps[0], caps[0]))
+                    w = wss[b % 2]
+                    if done[b % 2] is not None:
+                        main.wait_event(done[b % 2])  # the side stream is done reading this workspace
+                    nat.check(L.mgn_block_backward_data(*args, nat.ptr(w), w.numel(), st))
+                    evd = torch.cuda.Event()
+                    evd.record(main)
+                    side.wait_event(evd)
+                    nat.check(L.mgn_block_backward_wgrad(*args, nat.ptr(w), w.numel(), nat._vp(side.cuda_stream)))
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    done[b % 2] = ev
+                    with torch.cuda.stream(side):
+                        ready(G, blo, bhi)
+                dx, de = dx1, de1
+            if conc and ENC_DATA_CAP:
+                # the encoders' backward runs beside block 0's ring launch: its weight-gradient launches take
+                # the data share of the chip too (capped at the ring's share they took 63 instead of ~40 us)
+                nat.check(L.mgn_set_grid_cus(caps[0], caps[0]))
 
-        def join():  # the side stream's weight gradients are complete before their reduction
-            if conc:
-                nat.check(L.mgn_set_grid_cus(0, 0))
+            def join():  # the side stream's weight gradients are complete before their reduction
+                if conc:
+                    nat.check(L.mgn_set_grid_cus(0, 0))
+                    for ev in done:
+                        if ev is not None:
+                            main.wait_event(ev)
+
+            if defer and not defer_dense and (GRAD_READY is None or conc):
+                join()
+                if not side_reduced:
+                    nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
+            if overlap:
                 for ev in done:
                     if ev is not None:
-                        main.wait_event(ev)
-
-        side_reduced = conc and SIDE_REDUCE  # the processor blocks' slabs are reduced already
-        if defer and GRAD_READY is None and not defer_dense:
-            join()
-            if not side_reduced:
-                nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
-        if overlap:
-            for ev in done:
-                if ev is not None:
-                    main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
-        gx = gea = None
-        nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
-        if ctx.only_processor:
-            h = plan.specs[0].hidden
-            if nx:
-                gx = dx[:, :h].float().contiguous()
-            if nea:
-                gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous()
-        else:
-            ne, ee = plan.specs[0], plan.specs[1]
-            gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
-            gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
-            if defer_dense:
-                _mlp_bwd_deferred(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
-                                  ctypes.c_void_p(gp + 4 * off[0]), ws, keeps[1], ctypes.pointer(dreds[1]), st)
-                _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
-                                  nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
-                                  ctypes.pointer(dreds[2]), st)
-                join()
-                # ONE reduction for the whole model: decoder, every processor block, encoders
-                npr = 2 * nb if defer and not side_reduced else 0
-                allr = (nat.WgradReduce * (3 + npr))()
-                allr[0] = dreds[0]
-                for i in range(npr):
-                    allr[1 + i] = reds[i]
-                allr[len(allr) - 2], allr[len(allr) - 1] = dreds[1], dreds[2]
-                nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
+                        main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
+            gx = gea = None
+            nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+            if ctx.only_processor:
+                h = plan.specs[0].hidden
+                if nx:
+                    gx = dx[:, :h].float().contiguous()
+                if nea:
+                    gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous()
             else:
-                _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
-                         ctypes.c_void_p(gp + 4 * off[0]), ws, st)
-                _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
-                         nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
-            gx = gxc
-            if nea:
-                gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
-            ready(G, off[0], off[1] + plan.specs[1].numel)
+                ne, ee = plan.specs[0], plan.specs[1]
+                gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
+                gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
+                if defer_dense:
+                    _mlp_bwd_deferred(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc,
+                                      nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[0]), ws, keeps[1],
+                                      ctypes.pointer(dreds[1]), st)
+                    _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                                      nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
+                                      ctypes.pointer(dreds[2]), st)
+                    join()
+                    # ONE reduction for the whole model: decoder (unless reduced already), every processor
+                    # block (unless reduced on the side stream), encoders
+                    parts = ([] if early_dec else [dreds[0]]) + \
+                        ([reds[i] for i in range(2 * nb)] if defer and not side_reduced else []) + [dreds[1], dreds[2]]
+                    allr = (nat.WgradReduce * len(parts))(*parts)
+                    nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
+                else:
+                    _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
+                             ctypes.c_void_p(gp + 4 * off[0]), ws, st)
+                    _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                             nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
+                gx = gxc
+                if nea:
+                    gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
+                ready(G, off[0], off[1] + plan.specs[1].numel)
+        finally:
+            if conc:
+                L.mgn_set_grid_cus(0, 0)
         if plan.padded:
             G = plan.unpad(G)
             _grad_ready(G, 0, plan.numel)

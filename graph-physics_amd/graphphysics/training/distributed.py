@@ -90,13 +90,20 @@ class GradBuckets:
     it. finish() flushes the last bucket and joins the communication stream back into the compute
     stream. Every rank issues the same buckets in the same order (the backward is deterministic), as
     RCCL requires. Inside a hipGraph capture the collectives are recorded into the graph: one replay
-    then covers forward, backward, the overlapped all-reduces and the optimizer."""
+    then covers forward, backward, the overlapped all-reduces and the optimizer.
+
+    A range is final on the stream that is CURRENT when it is handed over — the compute stream, or
+    the side stream of the concurrent processor backward, whose weight-gradient launches and slab
+    reductions run beside the next block's data gradients (models/_engine.py). Each hand-over records
+    an event there, and a bucket's collective waits for the events of every range in it, so a bucket
+    merging ranges from both streams waits for exactly their producers."""
 
     def __init__(self, group=None, bucket_bytes=4 << 20):
         self.group = group
         self.bucket = int(bucket_bytes)
         self.comm = None
         self.cur = None  # (G, lo, hi)
+        self.events = {}  # open bucket: the latest hand-over event per producer stream
         self.issued = 0
         self.covered = 0  # elements handed over (TrainStep checks they are the whole buffer)
 
@@ -108,6 +115,10 @@ class GradBuckets:
         else:
             self._flush()
             self.cur = (G, lo, hi)
+        st = torch.cuda.current_stream(G.device)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        self.events[st.cuda_stream] = ev  # a later event on a stream covers the earlier ones
         if (self.cur[2] - self.cur[1]) * G.element_size() >= self.bucket:
             self._flush()
 
@@ -116,10 +127,11 @@ class GradBuckets:
             return
         G, lo, hi = self.cur
         self.cur = None
-        cur = torch.cuda.current_stream(G.device)
         if self.comm is None:
             self.comm = torch.cuda.Stream(device=G.device)
-        self.comm.wait_stream(cur)
+        for ev in self.events.values():
+            self.comm.wait_event(ev)
+        self.events = {}
         with torch.cuda.stream(self.comm):
             self._reduce(G[lo:hi])
         self.issued += 1

@@ -40,6 +40,7 @@ raise rewinds the host-side step count and LR schedule by the updates the device
 that catches the error and skips the batch continues from the state the reference would have.
 """
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -48,6 +49,23 @@ from graphphysics import _native as nat
 from graphphysics.training.distributed import GradBuckets, allreduce_gradients, flat_grad_buffer
 from graphphysics.utils.loss import masked_mse
 from graphphysics.utils.nodetype import NodeType
+
+
+_CTL_GROUPS = {}
+
+
+def control_group(group=None):
+    """The host-side (gloo) group TrainStep agrees its per-step re-capture decision on: `group` itself
+    when it is a gloo group, else one gloo group over the same ranks, created once per process and rank
+    set. dist.new_group is a collective over the default group: the first call for a rank set must be
+    made by every rank of the world (ranks outside `group` included)."""
+    if dist.get_backend(group) == "gloo":
+        return group if group is not None else dist.group.WORLD
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else None
+    g = _CTL_GROUPS.get(ranks)
+    if g is None:
+        g = _CTL_GROUPS[ranks] = dist.new_group(ranks=list(ranks) if ranks is not None else None, backend="gloo")
+    return g
 
 
 class TrainStep:
@@ -78,14 +96,13 @@ class TrainStep:
             sim.set_process_group(group if group is not None else dist.group.WORLD)
         # captured data-parallel step: every rank must choose the same between copy-then-replay and a
         # re-capture (their collective sequences differ), so the choice is agreed on a host-side (gloo)
-        # control group — no device synchronisation, no extra collective on the GPU stream
+        # control group — no device synchronisation, no extra collective on the GPU stream. Creating it
+        # is a collective over the default group the first time a rank set is seen (control_group):
+        # every rank of the world constructs its TrainStep(s) in the same order, as for any DDP model
         self._ctl = None
+        self.ctl_seconds = 0.0  # host time spent in the per-step agreement (bench reports it at N > 1)
         if self.dp and graph and self.world > 1:
-            if dist.get_backend(group) == "gloo":
-                self._ctl = group if group is not None else dist.group.WORLD
-            else:
-                ranks = dist.get_process_group_ranks(group) if group is not None else None
-                self._ctl = dist.new_group(ranks=ranks, backend="gloo")
+            self._ctl = control_group(group)
 
     @property
     def node_type(self):
@@ -219,6 +236,9 @@ class TrainStep:
         self.batch = Data(x=b.x.clone(), y=b.y.clone(), edge_attr=b.edge_attr.clone(), edge_index=b.edge_index,
                           **extra)
         snap = self._snapshot()
+        # the warm-up steps are undone on a bad batch, so is the divergence mark one of them may set
+        # (ADVICE r04): the recovery step below must run, and only ITS error marks the replicas
+        diverged = getattr(self, "_dp_diverged", None)
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
@@ -239,6 +259,7 @@ class TrainStep:
             torch.cuda.synchronize()
             nat.error_word(dev)._clear()
             self._restore(snap)
+            self._dp_diverged = diverged
             self.batch = b
             self.graph = None
             _engine.forget_topology(b.edge_index)  # its cached (clamped) topology would not re-flag it
@@ -258,7 +279,10 @@ class TrainStep:
         # no fallback: a failure to record the overlapped all-reduce raises on every rank (a rank that
         # silently re-recorded without it would issue a different collective sequence)
         g, loss = self._record()
-        self.graph, self.static_loss = g, loss
+        # the replay writes the loss into this tensor's storage; detached, it does not keep the recorded
+        # autograd graph alive — whose AccumulateGrad nodes carry the capture stream, so an eager step
+        # between replays reused them from another stream ("AccumulateGrad node's stream does not match")
+        self.graph, self.static_loss = g, loss.detach()
         self._graph_grads = [p.grad for p in self.params]
         self._gflat = flat_grad_buffer(self.params)
         b = self.batch
@@ -338,8 +362,10 @@ class TrainStep:
         if self._ctl is not None:
             # re-capture on every rank if any rank needs to (a rank that copies and
             # replays while another re-captures would pair mismatched collectives)
+            t0 = time.perf_counter()
             need = torch.tensor([1 if self.graph is None else 0], dtype=torch.int32)
             dist.all_reduce(need, op=dist.ReduceOp.MAX, group=self._ctl)
+            self.ctl_seconds += time.perf_counter() - t0
             if int(need[0]):
                 self.graph = None
         if self.graph is None:

@@ -38,12 +38,12 @@ def _retype(b, seed, frac):
     return b
 
 
-def _batches():
-    """The STEPS training batches (4 CylinderFlow graphs each): different frames, jitter and node
-    types every step, the same mesh (one edge_index)."""
+def _batches(graphs=4):
+    """The STEPS training batches (4 CylinderFlow graphs each; 8: Cfg B's batch): different frames,
+    jitter and node types every step, the same mesh (one edge_index)."""
     from graphphysics.utils import meshes
 
-    return [_retype(meshes.cylinder_batch(4, t=k, jitter=0.01, seed=1234 + k), 77 + k, 0.03 + 0.04 * k)
+    return [_retype(meshes.cylinder_batch(graphs, t=k, jitter=0.01, seed=1234 + k), 77 + k, 0.03 + 0.04 * k)
             for k in range(STEPS)]
 
 
@@ -90,8 +90,10 @@ def _run(ds, dtype, mp_, h, data_parallel, graph=True, info=None):
         losses.append(float(st().item()))
     torch.cuda.synchronize()
     if info is not None:
+        from graphphysics.models import _engine
+
         info.update(overlap=bool(st.overlap), issued=st.buckets.issued if st.buckets is not None else 0,
-                    graph=st.graph is not None)
+                    graph=st.graph is not None, schedule=dict(_engine.LAST_SCHEDULE))
     return losses, [p.detach().float().cpu().clone() for p in sim.parameters()], \
         [b.detach().cpu().clone() for b in sim.buffers()], grads
 
@@ -168,7 +170,7 @@ def test_two_rank_libmgn_step_equals_single_process(dtype, mp_, h, graph):
         torch.testing.assert_close(b0, bb, rtol=1e-5, atol=1e-5)
 
 
-def _worker_rccl(rank, world, port, out, dtype, mp_, h):
+def _worker_rccl(rank, world, port, out, dtype, mp_, h, graphs=4):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "graph-physics_amd")]
     # 1 MiB buckets: several per step (the decoder alone, groups of processor blocks, the encoders)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MGN_GRAD_BUCKET_MB="1")
@@ -178,32 +180,41 @@ def _worker_rccl(rank, world, port, out, dtype, mp_, h):
 
     ge.build()
     info = {}
-    losses, params, bufs, grads = _run([{k: b[k] for k in ("x", "y", "edge_index", "edge_attr")} for b in _batches()],
-                                       dtype, mp_, h, True, True, info)
+    losses, params, bufs, grads = _run([{k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}
+                                        for b in _batches(graphs)], dtype, mp_, h, True, True, info)
     torch.save({"losses": losses, "params": params, "bufs": bufs, "grads": grads, "info": info},
                os.path.join(out, "rccl.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,mp_,h", [(torch.float32, 3, 32), (torch.bfloat16, 4, 128)])
-def test_rccl_overlapped_allreduce_step_equals_single_process(dtype, mp_, h):
+@pytest.mark.parametrize("dtype,mp_,h,graphs", [(torch.float32, 3, 32, 4), (torch.bfloat16, 4, 128, 4),
+                                                 (torch.bfloat16, 15, 128, 8)])
+def test_rccl_overlapped_allreduce_step_equals_single_process(dtype, mp_, h, graphs):
     """The RCCL data-parallel step records the bucketed gradient all-reduce (overlapped with the
     backward on a communication stream) and AdamW inside the hipGraph (training/step.py,
     distributed.GradBuckets). On a 1-rank RCCL group every all-reduce is the identity, so the step
     must equal the single-process captured step exactly: same losses, gradients and parameters
     bit for bit (a missed or doubled bucket, or a bucket reduced before its gradients were written,
-    shows up here). Run in a child process (one RCCL communicator, torn down with the process)."""
+    shows up here). Run in a child process (one RCCL communicator, torn down with the process).
+    graphs=8 is Cfg B (MP15/h128 bf16, 8 CylinderFlow graphs): the concurrent processor backward
+    (MGN_CONC_WGRAD=auto) runs under the bucketed all-reduce, each block's range handed over on the
+    side stream after its slab reduction, the decoder's right after its weight gradients."""
     import __graft_entry__ as ge
 
     ge.build()
-    port = 30600 + os.getpid() % 500 + (0 if dtype == torch.float32 else 500)
+    port = 30600 + os.getpid() % 500 + (0 if dtype == torch.float32 else 500) + (0 if graphs == 4 else 1000)
     with tempfile.TemporaryDirectory() as out:
-        mp.start_processes(_worker_rccl, args=(1, port, out, dtype, mp_, h), nprocs=1, join=True, start_method="spawn")
+        mp.start_processes(_worker_rccl, args=(1, port, out, dtype, mp_, h, graphs), nprocs=1, join=True,
+                           start_method="spawn")
         r = torch.load(os.path.join(out, "rccl.pt"), weights_only=True)
     # the overlapped all-reduce was recorded (TrainStep has no silent fallback), in several buckets
     assert r["info"]["overlap"] and r["info"]["graph"] and r["info"]["issued"] >= 2, r["info"]
-    losses, params, bufs, grads = _run([{k: b[k] for k in ("x", "y", "edge_index", "edge_attr")} for b in _batches()],
-                                       dtype, mp_, h, False)
+    sched = r["info"]["schedule"]
+    assert sched["grad_ready"], sched
+    if graphs == 8:  # Cfg B: the concurrent backward ran under the bucketed all-reduce
+        assert sched["conc"] is not None and sched["side_reduced"] and sched["early_dec"], sched
+    losses, params, bufs, grads = _run([{k: b[k] for k in ("x", "y", "edge_index", "edge_attr")}
+                                        for b in _batches(graphs)], dtype, mp_, h, False)
     assert r["losses"] == losses
     for a, c in zip(r["grads"], grads):
         assert torch.equal(a, c)

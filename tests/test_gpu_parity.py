@@ -730,6 +730,8 @@ def test_block_edge_attr_fp16_and_fp64_inputs():
 def test_eager_between_replays_keeps_graph_gradients():
     """eager() or zero_grad(set_to_none) between replays must not leave the captured
     step's all-reduce + AdamW reading stale or missing gradients (1-rank data-parallel step)."""
+    import warnings
+
     import torch.distributed as dist
 
     from graphphysics.training.step import TrainStep
@@ -740,18 +742,24 @@ def test_eager_between_replays_keeps_graph_gradients():
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
         for mix in (False, True):
-            sim, opt, sch, data = _cyl_train_setup(torch.float32)
-            st = TrainStep(sim, opt, sch, data, graph=True, data_parallel=True)
-            ref = TrainStep(sim, opt, sch, data, graph=False, data_parallel=True)
-            losses = []
-            for i in range(6):
-                if mix and i in (2, 4):
-                    losses.append(float(ref().item()))  # an eager step between replays
-                    opt.zero_grad(set_to_none=True)
-                else:
-                    losses.append(float(st().item()))
-            torch.cuda.synchronize()
+            with warnings.catch_warnings(record=True) as caught:
+                warnings.simplefilter("always")
+                sim, opt, sch, data = _cyl_train_setup(torch.float32)
+                st = TrainStep(sim, opt, sch, data, graph=True, data_parallel=True)
+                ref = TrainStep(sim, opt, sch, data, graph=False, data_parallel=True)
+                losses = []
+                for i in range(6):
+                    if mix and i in (2, 4):
+                        losses.append(float(ref().item()))  # an eager step between replays
+                        opt.zero_grad(set_to_none=True)
+                    else:
+                        losses.append(float(st().item()))
+                torch.cuda.synchronize()
             res.append((losses, [p.detach().clone() for p in sim.parameters()]))
+            # the eager step must not reuse the captured step's AccumulateGrad nodes, recorded on the
+            # capture stream ("AccumulateGrad node's stream does not match")
+            bad = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
+            assert not bad, bad[:1]
     finally:
         dist.destroy_process_group()
     np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-5)

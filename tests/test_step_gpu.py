@@ -41,12 +41,15 @@ def _batch(t=0, nb=2, seed=1234):
     return Data(**{k: torch.from_numpy(b[k]).to(DEV) for k in ("x", "y", "edge_index", "edge_attr")})
 
 
+@pytest.mark.parametrize("conc", ["0", "160,96"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype):
+def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype, conc, monkeypatch):
     """A GradBuckets whose collective DOUBLES its bucket on the communication stream, recorded in a
     hipGraph with the backward: the replayed gradients must be exactly 2x the plain backward's
     (a doubled bucket gives 4x, a missed one 1x, one issued before its producer finished leaves the
-    producer's 1x values)."""
+    producer's 1x values). conc "160,96": the concurrent processor backward (each block's weight
+    gradients and slab reduction on the side stream beside the next block's data half, the decoder's
+    weight gradients beside the last block's), whose ranges are handed over on the side stream."""
     from graphphysics.models import _engine
     from graphphysics.training.distributed import GradBuckets
     from graphphysics.utils.loss import masked_mse
@@ -55,6 +58,7 @@ def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype):
         def _reduce(self, t):
             t.mul_(2.0)
 
+    monkeypatch.setattr(_engine, "CONC_WGRAD", conc)
     sim = _model(dtype)
     sim.train()
     data = _batch()
@@ -88,6 +92,9 @@ def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype):
             _engine.GRAD_READY = None
         buckets.finish()
     assert buckets.covered == sum(p.numel() for p in params) and buckets.issued >= 2
+    sched = dict(_engine.LAST_SCHEDULE)
+    assert (sched["conc"] is not None) == (conc != "0") and sched["grad_ready"], sched
+    assert sched["early_dec"] == (conc != "0"), sched
     gg = [p.grad for p in params]
     state = [b.detach().clone() for b in sim.buffers()]
     g.replay()
@@ -104,7 +111,7 @@ def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype):
         assert torch.equal(a, 2.0 * p.grad), (float((a - 2 * p.grad).abs().max()), float(p.grad.abs().max()))
 
 
-def _train(graph, dtype=torch.bfloat16):
+def _train(graph, dtype=torch.bfloat16, dp=None):
     from graphphysics.training.optim import FusedAdamW
     from graphphysics.training.step import TrainStep
     from graphphysics.utils.scheduler import CosineWarmupScheduler
@@ -113,7 +120,7 @@ def _train(graph, dtype=torch.bfloat16):
     sim.train()
     opt = FusedAdamW(sim.parameters(), lr=1e-3, weight_decay=1e-4, betas=(0.9, 0.95))
     sch = CosineWarmupScheduler(opt, warmup=3, max_iters=40)
-    st = TrainStep(sim, opt, sch, _batch(), graph=graph)
+    st = TrainStep(sim, opt, sch, _batch(), graph=graph, data_parallel=dp)
     return sim, opt, sch, st
 
 
@@ -208,6 +215,40 @@ def test_bad_edge_index_skips_the_optimizer_update(graph):
         (before["step_count"], before["lr"], before["last_epoch"])
     # the bad step's own preamble accumulated (before the topology build flagged the index)
     assert float(after["node_norm"]["_acc_count"] - before["node_norm"]["_acc_count"]) == float(good.x.shape[0])
+
+
+def test_data_parallel_graph_bad_edge_index_raises_index_error():
+    """a data-parallel captured step whose re-capture warm-up meets a bad edge_index must
+    undo the warm-up (its divergence mark included), run the batch once eagerly and raise the
+    reference's IndexError — not the 'replicas differ' RuntimeError the warm-up's own mark would
+    trigger — leaving parameters and moments untouched; only then does the step refuse to continue.
+    A 1-rank gloo group with the multi-rank divergence bookkeeping (world = 2) on one GPU."""
+    import torch.distributed as dist
+    from graphphysics.utils.data import Data
+
+    dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
+    try:
+        sim, opt, sch, st = _train(True, dp=True)
+        st.world = 2  # divergence bookkeeping of a multi-rank job; the collectives stay 1-rank
+        good = st.batch
+        st()
+        torch.cuda.synchronize()
+        before = _state(sim, opt, sch)
+        ei = good.edge_index.clone()
+        ei[0, 3] = good.x.shape[0] + 5
+        st.batch = Data(x=good.x, y=good.y, edge_index=ei, edge_attr=good.edge_attr)
+        with pytest.raises(IndexError):
+            for _ in range(3):
+                st()
+                torch.cuda.synchronize()
+        after = _state(sim, opt, sch)
+        for k in ("params", "moments"):
+            assert _same(after[k], before[k]), k
+        st.batch = good
+        with pytest.raises(RuntimeError, match="replicas"):
+            st()
+    finally:
+        dist.destroy_process_group()
 
 
 def test_new_batch_in_graph_mode_is_replayed():

@@ -7,7 +7,8 @@ counters of the same kernel instance, build and workload.
   MFMA:      SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over SIMDs) and GRBM_GUI_ACTIVE (GPU-busy cycles
              summed over the 8 XCDs): mfma_util = MFMA_BUSY / (SIMDs x GRBM_GUI_ACTIVE / 8).
 
-    python tools/pmc_traffic.py <workload> <out.json> <fetch.csv> <write.csv> [<sq.csv>]
+    python tools/pmc_traffic.py <workload> <out.json> <fetch.csv> <write.csv> [<sq.csv> [<trace.csv> <steps>
+                                [<pmc_trace.csv> <schedule>]]]
 """
 import csv
 import hashlib
@@ -84,8 +85,25 @@ def replay_classes(trace_csv, steps):
                 "avg_us": round(sum(v) / len(v), 2)} for c, v in agg.items()}
 
 
-def main(workload, out, fetch_csv, write_csv, sq_csv=None, trace_csv=None, steps=5):
+def trace_durations(trace_csv):
+    """{instance: median duration in us} of every training-step kernel launch in a kernel trace."""
+    per = {}
+    for r in csv.DictReader(open(trace_csv)):
+        if kernel_class(r["Kernel_Name"]) is None:
+            continue
+        key = "%s|grid=%s" % (r["Kernel_Name"], r.get("Grid_Size", r.get("Grid_Size_X", "")))
+        per.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {k: statistics.median(v) for k, v in per.items()}
+
+
+def main(workload, out, fetch_csv, write_csv, sq_csv=None, trace_csv=None, steps=5, pmc_trace_csv=None,
+         schedule=None):
+    """pmc_trace_csv: a kernel trace of the bench command run with the SAME schedule as the PMC passes
+    (profile_round.sh: one stream, MGN_CONC_WGRAD=0), so every PMC record carries the duration of its own
+    launches (`trace_us`) and the clock its GRBM_GUI_ACTIVE implies over them; trace_csv (the default
+    schedule) gives the replayed step's per-class times."""
     f, w, q = load(fetch_csv), load(write_csv), load(sq_csv)
+    durs = trace_durations(pmc_trace_csv) if pmc_trace_csv else {}
     res = {}
     for key in sorted(set(f) | set(w) | set(q)):
         name = key.split("|grid=")[0]
@@ -101,9 +119,16 @@ def main(workload, out, fetch_csv, write_csv, sq_csv=None, trace_csv=None, steps
             d[c] = statistics.median(v)
         if "SQ_VALU_MFMA_BUSY_CYCLES" in d and d.get("GRBM_GUI_ACTIVE"):
             d["mfma_util"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * d["GRBM_GUI_ACTIVE"] / XCDS)
+        if d.get("GRBM_GUI_ACTIVE"):
+            d["grbm_us_at_2400MHz"] = round(d["GRBM_GUI_ACTIVE"] / XCDS / 2400.0, 2)
+        if key in durs:
+            d["trace_us"] = round(durs[key], 2)
+            if d.get("GRBM_GUI_ACTIVE"):
+                d["implied_clock_mhz"] = round(d["GRBM_GUI_ACTIVE"] / XCDS / durs[key], 0)
         res[key] = d
     doc = {"sources_sha": sources_sha(), "workload": workload, "fetch_correction": 2.0,
-           "unit": "per launch (median over launches)", "kernels": res}
+           "unit": "per launch (median over launches)", "kernels": res,
+           "schedule": schedule or "default (MGN_CONC_WGRAD=auto)"}
     if trace_csv:
         doc["replay"] = replay_classes(trace_csv, int(steps))
         doc["replay_source"] = "rocprofv3 --kernel-trace of the same bench command, last %s replayed steps" % steps
