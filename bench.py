@@ -524,8 +524,9 @@ def main():
         "data": "synthetic: %s, random-init weights (seed 0)" % datadesc,
         "execution": ("eager, a new batch (fresh x / y / edge_index / edge_attr tensors, topology rebuilt) "
                       "every step" if a.fresh_batch else "eager" if not step.use_graph else
-                      ("statistics + mask-count all-reduce, then hipGraph replay of forward+loss+backward with "
-                       "the bucketed gradient all-reduce overlapped on a communication stream + AdamW"
+                      ("hipGraph replay of the whole data-parallel step: statistics + mask-count all-reduce, "
+                       "forward+loss+backward with the bucketed gradient all-reduce overlapped on a communication "
+                       "stream, AdamW"
                        if step.overlap else
                        "hipGraph replay of forward+loss+backward; eager statistics/gradient all-reduce + AdamW")
                       if step.dp else "hipGraph replay of the whole step"),

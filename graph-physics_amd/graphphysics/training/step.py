@@ -9,16 +9,17 @@ Captured mode (single process): the whole forward + backward + AdamW launch sequ
 is recorded once into a hipGraph and replayed; per step the host only writes {lr, step} to the
 device and calls replay(), so host/launch overhead disappears. Requires a static batch (the bench's
 resident synthetic meshes, or a training loop that copies each batch into the same buffers).
-Data parallel (process group of >1 rank), captured: the three exchanges of
-graphphysics.training.distributed stay outside the graph — the normalizer batch statistics depend
-only on the batch, so Simulator.exchange_statistics() sums them over ranks (one packed all-reduce)
-before the replay; the global masked-node count is fixed per batch; the replay covers forward,
-loss and backward; then ONE all-reduce of the flat gradient buffer and the AdamW launch. Over RCCL
-(backend "nccl") the gradient all-reduce is instead bucketed and overlapped with the backward inside
-the graph (distributed.GradBuckets: the decoder's and each block's gradients are all-reduced on a
-communication stream as soon as the backward has produced them), and AdamW is recorded too: one
-replay per step after the statistics exchange. MGN_GRAD_OVERLAP=0 keeps the all-reduce after the
-replay. `graph=False`: the same exchanges, fully eager.
+Data parallel (process group of >1 rank), captured: three exchanges (graphphysics.training.distributed)
+— the normalizer batch statistics and the global masked-node count, summed over ranks in ONE packed
+all-reduce by Simulator.exchange_statistics() (they depend only on the batch, so exchanging them before
+the forward is exact), and the parameter gradients. Over RCCL (backend "nccl") all of it is recorded in
+the graph: the statistics launch and its all-reduce, the forward, the backward with the gradient
+all-reduce bucketed and overlapped on a communication stream (distributed.GradBuckets: the decoder's
+and each block's gradients are all-reduced as soon as the backward has produced them — on the
+concurrent processor backward, as soon as the side stream has reduced each block's slabs), and AdamW:
+one replay per step. Over gloo (not capturable) the statistics exchange runs before the replay and ONE
+all-reduce of the flat gradient buffer + AdamW after it; MGN_GRAD_OVERLAP=0 does the same over RCCL.
+`graph=False`: the same exchanges, fully eager.
 
 capture() warms the allocator and the library up with `warmup` eager steps and then RESTORES every
 piece of state they touched (parameters, optimizer moments and step count, scheduler, learning rate,
@@ -184,7 +185,7 @@ class TrainStep:
         self.opt.step()
         nat.error_word(self.batch.x.device).arm()  # the copy-back carries the optimizer's skip count
         self.sched.step()
-        return loss
+        return loss.detach()  # the backward ran: the caller gets the value, not the autograd graph
 
     def _snapshot(self):
         """Everything an eager step mutates: parameters + buffers (normalizer accumulators), the
@@ -275,7 +276,8 @@ class TrainStep:
         self.opt.zero_grad(set_to_none=True)
         if on_record is not None:
             on_record()
-        self._prologue()  # pending statistics exist before recording (the graph reads their buffers)
+        if not self.overlap:
+            self._prologue()  # pending statistics exist before recording (the graph reads their buffers)
         # no fallback: a failure to record the overlapped all-reduce raises on every rank (a rank that
         # silently re-recorded without it would issue a different collective sequence)
         g, loss = self._record()
@@ -316,6 +318,10 @@ class TrainStep:
         # "global" capture mode would turn that query into hipErrorStreamCaptureUnsupported (abort)
         mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
         with torch.cuda.graph(g, capture_error_mode=mode):
+            if self.overlap:
+                # RCCL: the statistics exchange (one statistics launch, the mask count, ONE all-reduce) is
+                # recorded too — it depends only on the batch the graph reads — so a step is ONE replay
+                self._prologue()
             loss = self._loss()
             if self.overlap:
                 from graphphysics.models import _engine
@@ -373,8 +379,7 @@ class TrainStep:
         self._bind_graph_grads()
         self.opt.stage()
         if self.dp and self.overlap:
-            self._prologue()
-            self.graph.replay()  # backward-overlapped gradient all-reduce + AdamW inside
+            self.graph.replay()  # statistics exchange, backward-overlapped gradient all-reduce + AdamW inside
         elif self.dp:
             self._prologue()
             self.graph.replay()

@@ -100,7 +100,9 @@ def test_captured_bucket_hook_sees_every_range_once_after_its_producer(dtype, co
     g.replay()
     torch.cuda.synchronize()
     got = [t.detach().clone() for t in gg]
-    # the same step without the hook, from the same normaliser state
+    # the same step without the hook, from the same normaliser state (the recorded graph's loss is
+    # dropped first: its AccumulateGrad nodes carry the capture stream)
+    del lv
     with torch.no_grad():
         for b, v in zip(sim.buffers(), state):
             b.copy_(v)
