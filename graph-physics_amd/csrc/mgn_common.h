@@ -123,14 +123,18 @@ __host__ __device__ __forceinline__ int rup(int a, int b) { return cdiv(a, b) * 
 // fragments of either region (the register-chained fp32 edge kernels' LDS-DMA source, mgn_mlp.hip):
 //   image[((nt*8 + t)*64 + lane)*4 + r]  = W[nt*16 + (lane&15)][t*16 + 4*(lane>>4) + r]   (forward)
 //   imageT[((kt*8 + t)*64 + lane)*4 + r] = W[t*16 + 4*(lane>>4) + r][kt*16 + (lane&15)]   (transposed)
-__host__ __device__ inline bool has_chain_image(int n, int k, int dtype) {
-    return dtype == MGN_F32 && n == 128 && k > 0 && k % 128 == 0;
+// — one such image per 128-column block of the input (round 5: the chained fp32 node MLP's layer 0
+// reads both blocks of its [x ‖ aggr] weight, the next block's projections the x_i / x_j blocks of the
+// edge W0), block b's image of columns 128b .. 128b + 127 at chain_image_off(n, k, b) (mgn_mlp.hip).
+__host__ __device__ inline int chain_images(int n, int k, int dtype) {
+    return dtype == MGN_F32 && n == 128 && k > 0 && k % 128 == 0 ? k / 128 : 0;
 }
+__host__ __device__ inline bool has_chain_image(int n, int k, int dtype) { return chain_images(n, k, dtype) > 0; }
 __host__ __device__ inline int64_t linear_pack_elems(int n, int k, int dtype) {
     const int vec = dtype == MGN_BF16 ? 8 : 1, kstep = 4 * vec;
     int64_t fwd = (int64_t)cdiv(n, 16) * cdiv(k, kstep);
     int64_t bwd = (int64_t)rup(cdiv(k, 16), 8) * cdiv(n, kstep);
-    return (fwd > bwd ? fwd : bwd) * 64 * vec + (has_chain_image(n, k, dtype) ? 128 * 128 : 0);
+    return (fwd > bwd ? fwd : bwd) * 64 * vec + (int64_t)chain_images(n, k, dtype) * 128 * 128;
 }
 
 // Layer shapes of build_mlp(in, hidden, out, L)

@@ -346,6 +346,10 @@ struct FwdArgs {
     int32_t r0_elems;  // LDS region 0 (layer-0 input / odd-layer activations / fp32 z staging), in T
     int32_t wl_elems;  // WL kernels: LDS element offset of the staged weights
     WlDesc wl;
+    // chained fp32 node MLP: the NEXT block's node projections P = [x_out·W0bᵀ ‖ x_out·W0cᵀ] (fp32
+    // [N][2H], what node_proj_kernel writes) from the next edge MLP's forward pack (nullptr: none)
+    const float* pn_pack;
+    float* pn_out;
 };
 
 // Diagnostic ablation mask for timing studies (results are wrong when nonzero): a compile-time
@@ -1754,15 +1758,16 @@ __device__ __forceinline__ void pack_job(const mgn_pack_job& j) {
     // one Linear's pack is far below 2^31 elements: 32-bit index math (64-bit divisions by the
     // runtime KS / NS cost tens of instructions each)
     const int tot = (int)linear_pack_elems(n, k, dtype_id<T>());
-    const int img0 = has_chain_image(n, k, dtype_id<T>()) ? tot - 128 * 128 : tot;  // chain image start
+    const int img0 = tot - chain_images(n, k, dtype_id<T>()) * 128 * 128;  // chain images start
     T* dst = reinterpret_cast<T*>(j.dst);
     T* dstT = reinterpret_cast<T*>(j.dstT);
     for (int e = blockIdx.x * MGN_THREADS + threadIdx.x; e < tot; e += gridDim.x * MGN_THREADS) {
-        if (e >= img0) {  // chain images (mgn_common.h): first 128 input columns, permuted k-steps
-            const int i = e - img0, r = i & 3, lane = (i >> 2) & 63, t = (i >> 8) & 7, b = i >> 11;
+        if (e >= img0) {  // chain images (mgn_common.h): one per 128-column block, permuted k-steps
+            const int i = e - img0, r = i & 3, lane = (i >> 2) & 63, t = (i >> 8) & 7, b = (i >> 11) & 7;
+            const int cb = 128 * (i >> 14);  // the image's first input column
             const int a16 = b * 16 + (lane & 15), c = t * 16 + 4 * (lane >> 4) + r;
-            dst[e] = from_f<T>(pack_src(j, a16, c));   // W[a16][c]
-            dstT[e] = from_f<T>(pack_src(j, c, a16));  // W[c][a16]
+            dst[e] = from_f<T>(pack_src(j, a16, cb + c));   // W[a16][cb + c]
+            dstT[e] = from_f<T>(pack_src(j, c, cb + a16));  // W[c][cb + a16]
             continue;
         }
         const int v = e % VEC;
@@ -1825,10 +1830,11 @@ constexpr int F32C_NBUF = MGN_F32C_SB ? 1 : 2;    // LDS chain images per workgr
 #define F32C_BOUNDS __launch_bounds__(F32C_WAVES * 64, 3)
 constexpr int F32C_LAYER = 128 * 128;  // floats per chain image (64 KiB)
 
-// The chain image of a pack region (fwd or transposed) of a fp32 [n][k] Linear, or NULL: it follows
-// the fragments (linear_pack_elems counts it: n == 128, k a multiple of 128).
-__host__ __device__ inline int64_t chain_image_off(int n, int k) {
-    return linear_pack_elems(n, k, MGN_F32) - F32C_LAYER;
+// The chain image of input columns 128b .. 128b + 127 in a pack region (fwd or transposed) of a fp32
+// [n][k] Linear: the images follow the fragments (linear_pack_elems counts them: n == 128, k a multiple
+// of 128, one per 128-column block).
+__host__ __device__ inline int64_t chain_image_off(int n, int k, int b = 0) {
+    return linear_pack_elems(n, k, MGN_F32) - (int64_t)(chain_images(n, k, MGN_F32) - b) * F32C_LAYER;
 }
 
 // Issue this wave's share of one 64 KiB image copy global -> LDS (1 KiB per LDS-DMA instruction).
@@ -2227,6 +2233,330 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
     F32C_STAMP_PRINT("f32b");
 }
 
+// --------------------------------------------------------------------------- fp32 node MLP, register-chained
+// The fp32 GraphNetBlock node MLP at h = 128 (round 5; reference layers.py:660-665, 694-699, 733-746:
+// [x ‖ Σ_in-edges m] -> 4 Linears -> RMSNorm, + x): the edge MLP's fp32 chain (f32c_gemm: each wave owns
+// 16 rows through all layers, activations never leave registers, the C layout of layer l is the B
+// operand of layer l+1) with ONE wave per SIMD — N is ≈ E/5.8, so the edge kernels' 12-wave workgroups
+// would fill a third of the chip, and a wave alone on its SIMD keeps the MFMA pipe fed from 8
+// independent accumulators. The aggregation of the in-edges' messages s_e ⊙ z_k / q_k (target-sorted
+// segments, edge order: the reference scatter_add's order, the generic kernel's expression, so the
+// aggregates are bit-identical to it) lands straight in the B operand of layer 0's aggregate block.
+// Layer 0 is two chain images (x block, aggr block of W0 [H x 2H]) and layers 1..3 one each: five
+// images through the two LDS buffers by LDS-DMA, each staged under the previous one's MFMAs. Saves as
+// the generic node kernel (the fp32 ring's node jobs read them): aggregate rows, R8 inputs of layers
+// 1..3, ReLU ballot words, z and rden. The backward mirrors it: RMSNorm backward, layers 3..1, then
+// dx_part = dx' + dZ0·W0[:, :H] and d_aggr = dZ0·W0[:, H:] from the two transposed images of W0.
+#ifndef MGN_F32N_CHAIN
+#define MGN_F32N_CHAIN 1  // 0: the fp32 node MLP on the generic LDS-tiled kernels (A/B builds)
+#endif
+#ifndef MGN_F32N_AG
+#define MGN_F32N_AG 4  // in-edges gathered per round trip by the fp32 aggregation
+#endif
+#ifndef MGN_F32N_PROJ
+#define MGN_F32N_PROJ 1  // the chained fp32 node MLP computes the next block's projections (A/B builds: 0)
+#endif
+constexpr int F32N_WAVES = 4;  // one wave per SIMD, 64 rows per workgroup
+#define F32N_BOUNDS __launch_bounds__(F32N_WAVES * 64, 1)
+constexpr size_t F32N_LDS_FWD = (2 * F32C_LAYER + 5 * 128) * sizeof(float);
+constexpr size_t F32N_LDS_BWD = (2 * F32C_LAYER + F32N_WAVES * 128) * sizeof(float);
+
+// this wave's share of one 64 KiB chain image copy global -> LDS (1 KiB per LDS-DMA instruction)
+__device__ __forceinline__ void f32n_stage(const float* __restrict__ src, float* img) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = wave; c < F32C_LAYER / 256; c += F32N_WAVES)
+        glds16(src + c * 256 + lane * 4, img + c * 256);
+}
+
+// ReLU of a hidden layer's accumulators into the next B operand + the tile's 32 ballot words (word
+// nt*4 + r from lane nt*4 + r: the generic kernels' mask layout at h = 128), as the fp32 edge forward
+__device__ __forceinline__ unsigned long long f32c_relu(f4 (&x)[8], const f4 (&acc)[8], int lane) {
+    unsigned long long word = 0;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float v = fmaxf(acc[nt][r], 0.f);
+            x[nt][r] = v;
+            const unsigned long long bits = __ballot(v > 0.f);
+            if (lane == nt * 4 + r) word = bits;
+        }
+    }
+    return word;
+}
+
+__global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
+    constexpr int H = 128;
+    constexpr int AG = MGN_F32N_AG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* const img0 = reinterpret_cast<float*>(smem);
+    float* const img1 = img0 + F32C_LAYER;
+    float* const vec = img1 + F32C_LAYER;  // [5][H]: b0..b3, RMSNorm scale
+    const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15;
+    const int64_t tile = (int64_t)blockIdx.x * F32N_WAVES + (threadIdx.x >> 6);
+    const int64_t row = tile * 16 + ri;
+    const bool valid = row < a.M;
+    const float* pk = reinterpret_cast<const float*>(a.wpack);
+    // layer 0's two images land during phase A
+    f32n_stage(pk + chain_image_off(H, 2 * H, 0), img0);
+    f32n_stage(pk + chain_image_off(H, 2 * H, 1), img1);
+    pk += linear_pack_elems(H, 2 * H, MGN_F32);
+    for (int i = threadIdx.x; i < 5 * H; i += F32N_WAVES * 64) {
+        const int vl = i >> 7;
+        const float* vp = vl == 0 ? a.bias[0] : vl == 1 ? a.bias[1] : vl == 2 ? a.bias[2] : vl == 3 ? a.bias[3] : a.scale;
+        vec[i] = vp[i & (H - 1)];
+    }
+    // phase A: x rows (layer 0's x-block operand and the residual) and the aggregate (its aggr block)
+    const int64_t rowc = valid ? row : a.M - 1;
+    const float* x = reinterpret_cast<const float*>(a.seg[0].p);
+    f4 xr[8], ag[8], sc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        xr[t] = *reinterpret_cast<const f4*>(x + rowc * a.seg[0].ld + 16 * t + 4 * g);
+        sc[t] = ld4u(a.agg_scale + 16 * t + 4 * g);
+        ag[t] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    {
+        const int kb = a.seg_ptr[rowc], ke = valid ? a.seg_ptr[rowc + 1] : kb;
+        const float* z = reinterpret_cast<const float*>(a.agg_z);
+#pragma unroll 1
+        for (int k = kb; k < ke; k += AG) {  // every load of a group before its first add
+            f4 zz[AG][8];
+            float qq[AG];
+#pragma unroll
+            for (int u = 0; u < AG; ++u) {
+                const int64_t ku = k + u < ke ? k + u : ke - 1;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) zz[u][t] = *reinterpret_cast<const f4*>(z + ku * H + 16 * t + 4 * g);
+                qq[u] = a.agg_rden[ku];
+            }
+#pragma unroll
+            for (int u = 0; u < AG; ++u) {
+                if (k + u >= ke) break;
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) ag[t][r] += sc[t][r] * (zz[u][t][r] / qq[u]);
+            }
+        }
+    }
+    if (!valid) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xr[t] = f4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) st4(reinterpret_cast<float*>(a.agg_save) + row * H + 16 * t + 4 * g, ag[t]);
+    }
+    f32c_stage_wait();
+    __syncthreads();
+    f4 acc[8], x1[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) acc[nt] = *reinterpret_cast<const f4*>(vec + 16 * nt + 4 * g);
+    f32c_gemm(acc, xr, img0, lane);  // x block
+    __syncthreads();                 // every wave is done with img0
+    const float* nxt = pk + chain_image_off(H, H);
+    f32n_stage(nxt, img0);           // layer 1's image streams in under the aggregate block
+    pk += linear_pack_elems(H, H, MGN_F32);
+    f32c_gemm(acc, ag, img1, lane);  // aggr block
+    float* act = reinterpret_cast<float*>(a.act8);
+    const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
+    unsigned long long word = f32c_relu(x1, acc, lane);
+    if (lane < 32) a.mask[tile * 32 + lane] = word;
+    f32c_stage_wait();
+    __syncthreads();
+    // layers 1..3 (layer l on buffer (l + 1) & 1): layer l+1's image streams into the other buffer
+#pragma unroll 1
+    for (int l = 1; l < 4; ++l) {
+        float* cur = (l & 1) ? img0 : img1;
+        if (l < 3) {
+            f32n_stage(pk + chain_image_off(H, H), (l & 1) ? img1 : img0);
+            pk += linear_pack_elems(H, H, MGN_F32);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = *reinterpret_cast<const f4*>(vec + l * H + 16 * nt + 4 * g);
+        float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
+        if (l == 3 && a.pn_pack)  // the next block's W0b image streams in under the last layer
+            f32n_stage(a.pn_pack + chain_image_off(H, 3 * H, 1), img1);
+        f32c_gemm(acc, x1, cur, lane, sv + r8);  // its input's R8 save, under the MFMAs
+        if (l < 3) {
+            word = f32c_relu(x1, acc, lane);
+            if (lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
+            f32c_stage_wait();
+            __syncthreads();
+        }
+    }
+    // last Linear (bias in the accumulator): RMSNorm, residual x
+    float ss = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss += acc[nt][r] * acc[nt][r];
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    {
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        if (valid && g == 0) a.rden_save[row] = q;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + n);
+            f4 y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = s[r] * (acc[nt][r] / q);
+            y = xr[nt] + y;
+            if (valid) {
+                st4(reinterpret_cast<float*>(a.z_save) + row * H + n, acc[nt]);
+                st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
+            }
+            x1[nt] = valid ? y : f4{0.f, 0.f, 0.f, 0.f};  // x_out: the projections' B operand
+        }
+    }
+    if (!a.pn_pack) return;
+    // the NEXT block's node projections from x_out (reference layers.py:689-690,717 applied per node:
+    // [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]), W0b from img1, W0c from img0
+    f32c_stage_wait();
+    __syncthreads();  // W0b landed; every wave is done with img0 (layer 3)
+    f32n_stage(a.pn_pack + chain_image_off(H, 3 * H, 2), img0);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        f32c_gemm(acc, x1, half ? img0 : img1, lane);
+        if (valid) {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) st4(a.pn_out + row * (2 * H) + half * H + 16 * nt + 4 * g, acc[nt]);
+        }
+        if (half == 0) {
+            f32c_stage_wait();
+            __syncthreads();
+        }
+    }
+}
+
+__global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
+    constexpr int H = 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* const img0 = reinterpret_cast<float*>(smem);
+    float* const img1 = img0 + F32C_LAYER;
+    float* const red = img1 + F32C_LAYER;  // [F32N_WAVES][H] per-wave RMSNorm-scale partials
+    const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15, wave = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * F32N_WAVES + wave;
+    const int64_t row = tile * 16 + ri;
+    const bool valid = row < a.M;
+    const float* wt = reinterpret_cast<const float*>(a.wtpack);
+    const int64_t off1 = linear_pack_elems(H, 2 * H, MGN_F32);       // transposed pack offsets
+    const int64_t off2 = off1 + linear_pack_elems(H, H, MGN_F32), off3 = off2 + linear_pack_elems(H, H, MGN_F32);
+    f32n_stage(wt + off3 + chain_image_off(H, H), img0);  // W3ᵀ, then W2ᵀ: both buffers
+    f32n_stage(wt + off2 + chain_image_off(H, H), img1);
+    unsigned long long mw[3] = {0ull, 0ull, 0ull};
+    if (lane < 32) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) mw[l] = a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane];
+    }
+    // ---- dY = dx_out -> dZ3 (RMSNorm backward), as the fp32 edge backward
+    f4 dz[8], z[8], dv[8];
+    float q = 1.f;
+    {
+        const int64_t rowc = valid ? row : a.M - 1;
+        const float* dout = reinterpret_cast<const float*>(a.dout);
+        const float* zs = reinterpret_cast<const float*>(a.z_save);
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            dz[nt] = *reinterpret_cast<const f4*>(dout + rowc * a.dout_ld + n);
+            z[nt] = *reinterpret_cast<const f4*>(zs + rowc * H + n);
+        }
+        const float qv = a.rden_save[rowc];
+        if (valid) {
+            q = qv;
+        } else {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) dz[nt] = z[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) dv[nt] = dz[nt];  // dx_part = dx_out + dA0[:, :H]
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+        const f4 s = ld4u(a.scale + 16 * nt + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dot += s[r] * dz[nt][r] * z[nt][r];
+    }
+    dot += __shfl_xor(dot, 16);
+    dot += __shfl_xor(dot, 32);
+    const float rms = q - RMS_EPS;
+    const float coef = rms > 0.f ? dot / (q * q * rms) * (a.dinv * a.dinv) : 0.f;
+    const int r4 = 2 * (ri & 1) + ((ri >> 1) & 1);
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+        const f4 s = ld4u(a.scale + 16 * nt + 4 * g);
+        f4 dsc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float dy = dz[nt][r];
+            dsc[r] = dy * (z[nt][r] / q);
+            dz[nt][r] = s[r] * dy / q - z[nt][r] * coef;
+        }
+        const float dsum = f32c_row16_sum4(dsc, ri);
+        if (ri < 4) red[wave * H + 16 * nt + 4 * g + r4] = dsum;
+    }
+    f32c_stage_wait();
+    __syncthreads();
+    float* dz8 = reinterpret_cast<float*>(a.dz8);
+    const int64_t r8 = f32c_r8t(row, g);
+    if (!(wave & 1) && ri == 0) {  // partials per 32 rows (the generic node kernel's count)
+        const int64_t p = (int64_t)blockIdx.x * (F32N_WAVES / 2) + (wave >> 1);
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            *reinterpret_cast<f4*>(a.dscale_part + p * H + n) =
+                *reinterpret_cast<const f4*>(red + wave * H + n) + *reinterpret_cast<const f4*>(red + (wave + 1) * H + n);
+        }
+    }
+    // ---- layers 3..1 (images W3ᵀ img0, W2ᵀ img1, W1ᵀ img0), then W0ᵀ's x block (img1), aggr block (img0)
+    f4 acc[8];
+#pragma unroll 1
+    for (int i = 0; i < 5; ++i) {
+        float* cur = (i & 1) ? img1 : img0;
+        // the image after next streams into the buffer the previous step freed (barrier below)
+        if (i >= 1 && i <= 3) {
+            const float* src = i == 1 ? wt + off1 + chain_image_off(H, H)                  // W1ᵀ
+                             : i == 2 ? wt + chain_image_off(H, 2 * H, 0)                  // W0ᵀ, x block
+                                      : wt + chain_image_off(H, 2 * H, 1);                 // W0ᵀ, aggr block
+            f32n_stage(src, (i & 1) ? img0 : img1);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        const int l = 3 - i;  // dZ_l feeds this GEMM (i = 4: dZ0 again, the aggr block)
+        float* sv = i < 4 ? dz8 + (int64_t)l * a.RP * H + r8 : nullptr;
+        f32c_gemm(acc, dz, cur, lane, sv);
+        if (i < 3) {
+            const unsigned long long mine = l == 3 ? mw[2] : l == 2 ? mw[1] : mw[0];
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const unsigned long long wd =
+                        ((unsigned long long)__builtin_amdgcn_readlane((int)(mine >> 32), nt * 4 + r) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)mine, nt * 4 + r);
+                    dz[nt][r] = ((wd >> lane) & 1ull) && valid ? acc[nt][r] : 0.f;
+                }
+        } else if (i == 3 && valid) {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt)
+                st4(reinterpret_cast<float*>(a.o1) + row * H + 16 * nt + 4 * g, dv[nt] + acc[nt]);
+        } else if (i == 4 && valid) {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) st4(reinterpret_cast<float*>(a.o2) + row * H + 16 * nt + 4 * g, acc[nt]);
+        }
+        if (i < 4) {
+            f32c_stage_wait();
+            __syncthreads();
+        }
+    }
+}
+
 // --------------------------------------------------------------------------- host side
 #ifndef MGN_BF16_BM
 #define MGN_BF16_BM 64  // rows per workgroup of the generic bf16 dense / edge kernels (A/B builds: 32)
@@ -2285,6 +2615,9 @@ struct MlpIn {
     const float* proj;    // EDGE: node projections (see FwdArgs)
     const int32_t* proj_i;
     const int32_t* proj_j;
+    const float* pn_pack; // NODE, fp32 h=128: the next block's projections (FwdArgs), if the chained kernel runs
+    float* pn_out;
+    int* pn_done;         // set to 1 when they were computed
 };
 
 template <class T, int H, int MODE>
@@ -2345,6 +2678,28 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
             if (int e = set_lds((const void*)edge_fwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_FWD_EDGE, st);
             hipLaunchKernelGGL(edge_fwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
+            MGN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
+    if constexpr (sizeof(T) == 4 && H == 128 && MODE == MODE_NODE) {
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        const SrcSeg& s0 = a.seg[0];
+        if (MGN_F32N_CHAIN && a.L == 4 && a.has_norm && a.NOUT == H && a.nseg == 1 && !s0.idx && s0.dtype == MGN_F32 &&
+            s0.ncols == H && s0.coff == 0 && s0.ld % 4 == 0 && al16(s0.p) && a.K0 == 2 * H && a.Kpack0 == 2 * H &&
+            a.resid == s0.p && a.seg_ptr && a.agg_z && al16(a.agg_z) && a.agg_rden && a.agg_scale && a.agg_save &&
+            al16(a.agg_save) && al16(a.z_save) && al16(a.act8) && out_dtype == MGN_F32 && a.out_ld % 4 == 0 &&
+            al16(a.out) && !a.ablate) {
+            const int grid = (int)(rows_pad(M) / (16 * F32N_WAVES));
+            if (grid == 0) return 0;
+            if (int e = set_lds((const void*)node_fwd_f32_chain_kernel, F32N_LDS_FWD)) return e;
+            if (in.pn_pack && in.pn_out) {
+                a.pn_pack = in.pn_pack;
+                a.pn_out = in.pn_out;
+                if (in.pn_done) *in.pn_done = 1;
+            }
+            ProfScope ps(PROF_FWD_NODE, st);
+            hipLaunchKernelGGL(node_fwd_f32_chain_kernel, dim3(grid), dim3(F32N_WAVES * 64), F32N_LDS_FWD, st, a);
             MGN_LAUNCH_CHECK();
             return 0;
         }
@@ -2450,6 +2805,20 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
             if (int e = set_lds((const void*)edge_bwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_BWD_EDGE, st);
             hipLaunchKernelGGL(edge_bwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
+            MGN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
+    if constexpr (sizeof(T) == 4 && H == 128 && MODE == MODE_NODE) {
+        auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+        if (MGN_F32N_CHAIN && a.L == 4 && a.has_norm && a.NOUT == H && a.Kpack0 == 2 * H && a.dout_dtype == MGN_F32 &&
+            a.dout_ld % 4 == 0 && al16(a.dout) && al16(a.z_save) && al16(a.dz8) && al16(a.o1) && al16(a.o2) &&
+            al16(a.dscale_part) && BM == 32 && !a.din) {
+            const int grid = (int)(a.RP / (16 * F32N_WAVES));
+            if (grid == 0) return 0;
+            if (int e = set_lds((const void*)node_bwd_f32_chain_kernel, F32N_LDS_BWD)) return e;
+            ProfScope ps(PROF_BWD_NODE, st);
+            hipLaunchKernelGGL(node_bwd_f32_chain_kernel, dim3(grid), dim3(F32N_WAVES * 64), F32N_LDS_BWD, st, a);
             MGN_LAUNCH_CHECK();
             return 0;
         }
@@ -3646,7 +4015,8 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     float* proj = reinterpret_cast<float*>(ws);
     const bool chain = chain_eligible(edge);
     const float* b0 = chain ? edge->bias[0] : nullptr;  // the chained kernel takes b0 from P_i
-    MGN_REQUIRE(!proj_ready || chain, "proj_ready: the workspace holds bf16 projections of the chained path only");
+    MGN_REQUIRE(!proj_ready || chain || dt == MGN_F32,
+                "proj_ready: the workspace holds the projections of the chained bf16 path or of the fp32 node MLP");
     // Small graphs on the generic kernels (hidden <= 64): layer 0 as the reference's single K = 3h
     // product over the gathered [e ‖ x_i ‖ x_j] rows (layers.py:689-690) — the node-projection launch
     // would cost more than the 4h² FLOPs per edge it saves (cylinder.json / plate.json sizes)
@@ -3698,9 +4068,23 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     memset(&nin, 0, sizeof(nin));
     nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
     nin.nseg = 1;
+    // fp32 h=128: the chained node kernel also computes the next block's node projections (the next
+    // call skips its projection launch)
+    int pn_done = 0;
+    if (MGN_F32N_PROJ && dt == MGN_F32 && H == 128 && next_edge && next_ws && next_edge->dtype == MGN_F32 &&
+        next_edge->hidden == H &&
+        next_edge->in_dim == 3 * H && next_ws_bytes >= block_fwd_ws(t, next_edge) && t->num_nodes > 0 &&
+        t->num_edges > 0) {
+        nin.pn_pack = reinterpret_cast<const float*>(next_edge->wpack);
+        nin.pn_out = reinterpret_cast<float*>(next_ws);
+        nin.pn_done = &pn_done;
+    }
     // K0 = 2H: the aggregation fills columns [H, 2H) inside the kernel
-    return mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
-                       saved->aggr, st);
+    if (int r = mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
+                            saved->aggr, st))
+        return r;
+    if (pn_done && next_proj_ready) *next_proj_ready = 1;
+    return 0;
 }
 
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,

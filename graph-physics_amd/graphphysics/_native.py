@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 14  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 15  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1

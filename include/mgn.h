@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 14
+#define MGN_ABI_VERSION 15
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -151,6 +151,9 @@ typedef struct mgn_pack_job {
     int32_t n_src, k_src, kb_src, kb_pad, reserved;
 } mgn_pack_job;
 
+/* ABI v15: an fp32 Linear with n == 128 and k a multiple of 128 carries one 128x128 "chain image" per
+ * 128-column input block (v14: of the first block only) — the register-chained fp32 edge and node MLP
+ * kernels' LDS-DMA source; the count changes, the layout stays opaque to callers. */
 int64_t mgn_linear_pack_elems(int32_t n, int32_t k, int32_t dtype);
 int64_t mgn_mlp_pack_elems(const mgn_mlp* m); /* Σ over layers of mgn_linear_pack_elems */
 /* jobs: DEVICE array of njobs mgn_pack_job; max_elems = max over jobs of n*k. One launch. */

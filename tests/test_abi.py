@@ -90,12 +90,12 @@ int main(void) {
 def test_host_size_functions(lib):
     from graphphysics import _native as nat
 
-    assert lib.mgn_abi_version() == 14
+    assert lib.mgn_abi_version() == 15
     # fragment-packed Linear: max(fwd, transposed) fragment count x 64 lanes x VEC
     assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_BF16) == max(8 * 12, 24 * 4) * 64 * 8
     assert lib.mgn_linear_pack_elems(2, 128, nat.MGN_F32) == max(1 * 32, 8 * 1) * 64
-    # fp32 128-wide Linears also carry the 128x128 chain image of the fp32 edge kernels
-    assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_F32) == max(8 * 96, 24 * 32) * 64 + 128 * 128
+    # fp32 128-wide Linears also carry a 128x128 chain image per 128-column block (fp32 chained kernels)
+    assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_F32) == max(8 * 96, 24 * 32) * 64 + 3 * 128 * 128
     assert lib.mgn_linear_pack_elems(128, 100, nat.MGN_F32) == max(8 * 25, 8 * 32) * 64
     m = nat.Mlp()
     m.n_layers, m.in_dim, m.hidden, m.out_dim, m.has_norm, m.dtype = 4, 384, 128, 128, 1, nat.MGN_BF16
