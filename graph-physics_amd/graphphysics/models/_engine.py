@@ -550,7 +550,7 @@ class EPDFunction(torch.autograd.Function):
     specs[4+2b]. only_processor: specs are the blocks only."""
 
     @staticmethod
-    def forward(ctx, plan, mdt, only_processor, x, edge_attr, topo, *params):
+    def forward(ctx, plan, mdt, only_processor, grad_mode, x, edge_attr, topo, *params):
         dev = x.device
         st = nat.stream_ptr(dev)
         tdt = nat.torch_dtype(mdt)
@@ -558,7 +558,10 @@ class EPDFunction(torch.autograd.Function):
         pw.repack(st)
         descs = pw.descs
         N, E = topo.num_nodes, topo.num_edges
-        train = any(ctx.needs_input_grad)
+        # grad_mode: torch.is_grad_enabled() at the call (a Function's forward runs with grad disabled, and
+        # needs_input_grad reports the inputs' requires_grad even under torch.no_grad): no autograd
+        # graph -> inference (the chained bf16 blocks run mgn_block_forward's kernels without saves)
+        train = grad_mode and any(ctx.needs_input_grad)
         if only_processor:
             bspecs, bdescs = plan.specs, descs
             H = bspecs[0].width  # the kernels' width (zero-padded when != hidden_size)
@@ -850,7 +853,7 @@ class EPDFunction(torch.autograd.Function):
                     if ev is not None:
                         main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
             gx = gea = None
-            nx, nea = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+            nx, nea = ctx.needs_input_grad[4], ctx.needs_input_grad[5]
             if ctx.only_processor:
                 h = plan.specs[0].hidden
                 if nx:
@@ -891,7 +894,7 @@ class EPDFunction(torch.autograd.Function):
             G = plan.unpad(G)
             _grad_ready(G, 0, plan.numel)
         ctx.state = None
-        return (None, None, None, gx, gea, None, *plan.grad_views(G))
+        return (None, None, None, None, gx, gea, None, *plan.grad_views(G))
 
 
 # --------------------------------------------------------------------------- GraphNetBlock
@@ -899,7 +902,7 @@ class BlockFunction(torch.autograd.Function):
     """(x', e') = GraphNetBlock(x, edge_index, e) with edges in the CALLER's order."""
 
     @staticmethod
-    def forward(ctx, plan, mdt, x, edge_attr, topo, *params):
+    def forward(ctx, plan, mdt, grad_mode, x, edge_attr, topo, *params):
         dev = x.device
         st = nat.stream_ptr(dev)
         tdt = nat.torch_dtype(mdt)
@@ -916,7 +919,7 @@ class BlockFunction(torch.autograd.Function):
             raise ValueError(f"edge_attr must have shape [{E}, {h}], got {list(ea.shape)}")
         e0 = _permute(_padc(ea, H).contiguous(), topo.csc_eid, E, H, nat.mgn_dtype(ea.dtype), tdt, False, st) \
             if E else torch.empty((0, H), dtype=tdt, device=dev)
-        train = any(ctx.needs_input_grad)
+        train = grad_mode and any(ctx.needs_input_grad)  # as EPDFunction
         if not train and nat.lib().mgn_block_forward_inference_supported(ctypes.byref(pw.descs[0]),
                                                                          ctypes.byref(pw.descs[1])):
             sv = _alloc_block_infer(espec, topo, tdt, dev)
@@ -963,12 +966,12 @@ class BlockFunction(torch.autograd.Function):
             nat.ptr(e0), ctypes.byref(sv[0]), nat.ptr(dxo), nat.ptr(deo), nat.ptr(dx), nat.ptr(de),
             ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(G.data_ptr() + 4 * plan.offsets_pad[1]),
             nat.ptr(ws), ws.numel(), st))
-        gxo = dx[:, :h].to(ctx.xdtype).contiguous() if ctx.needs_input_grad[2] else None
+        gxo = dx[:, :h].to(ctx.xdtype).contiguous() if ctx.needs_input_grad[3] else None
         geo = None
-        if ctx.needs_input_grad[3]:
+        if ctx.needs_input_grad[4]:
             geo = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous() if E else \
                 torch.zeros((0, h), device=dev)
         if plan.padded:
             G = plan.unpad(G)
         ctx.state = None
-        return (None, None, gxo, geo, None, *plan.grad_views(G))
+        return (None, None, None, gxo, geo, None, *plan.grad_views(G))

@@ -231,5 +231,5 @@ class GraphNetBlock(nn.Module):
         nat.require_device(x)
         topo = _engine.get_topology(edge_index, x.size(0))
         plan = self._get_plan()
-        return _engine.BlockFunction.apply(plan, nat.mgn_dtype(self.compute_dtype), x, edge_attr, topo,
-                                           *plan.params)
+        return _engine.BlockFunction.apply(plan, nat.mgn_dtype(self.compute_dtype), torch.is_grad_enabled(), x,
+                                           edge_attr, topo, *plan.params)

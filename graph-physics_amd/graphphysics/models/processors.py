@@ -75,4 +75,4 @@ class EncodeProcessDecode(nn.Module):
         topo = _engine.get_topology(edge_index, x.size(0))
         plan = self._get_plan()
         return _engine.EPDFunction.apply(plan, nat.mgn_dtype(self.compute_dtype), self.only_processor,
-                                         x, edge_attr, topo, *plan.params)
+                                         torch.is_grad_enabled(), x, edge_attr, topo, *plan.params)

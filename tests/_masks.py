@@ -29,14 +29,14 @@ def _r8(act, off, rows, cols):
     return a[:rows]
 
 
-def _mlp_masks(spec, act, rows, gathered, kstep):
+def _mlp_masks(spec, act, rows, gathered, kstep, device="cpu"):
     """[bool [rows, hidden] per hidden layer] of one MLP from its saved act buffer."""
     rp = _rows_pad(rows)
     cols = _rup(spec.width, kstep)
     off = 0 if gathered else rp * _rup(spec.shapes[0][1], kstep)
     out = []
     for _ in range(1, spec.n_layers):
-        out.append((_r8(act, off, rows, cols)[:, :spec.hidden] > 0).cpu())
+        out.append((_r8(act, off, rows, cols)[:, :spec.hidden] > 0).to(device))
         off += rp * cols
     return out
 
@@ -44,10 +44,12 @@ def _mlp_masks(spec, act, rows, gathered, kstep):
 class MaskRecorder:
     """Install as graphphysics.models._engine.INSPECT; after a training forward, .masks holds the
     oracle-keyed masks {mlp prefix: [bool [rows, h]]} in the CALLER's row order (edge MLPs run in the
-    target-sorted order: mapped back through csc_eid)."""
+    target-sorted order: mapped back through csc_eid). device: where the masks are kept ("cpu", or the
+    GPU for graphs whose masks would not fit the host comfortably — Cfg E: 8 GB of them)."""
 
-    def __init__(self):
+    def __init__(self, device="cpu"):
         self.masks = None
+        self.device = device
 
     def __call__(self, st):
         from graphphysics import _native as nat
@@ -56,7 +58,8 @@ class MaskRecorder:
         torch.cuda.synchronize()
         plan, topo = st["plan"], st["topo"]
         N, E = topo.num_nodes, topo.num_edges
-        eid = topo.csc_eid[:E].long().cpu()
+        dev = self.device
+        eid = topo.csc_eid[:E].long().to(dev)
 
         def to_caller(ms):
             out = []
@@ -70,17 +73,53 @@ class MaskRecorder:
         ks = 4
         if not st["only_processor"]:
             ne, ee, dec = plan.specs[:3]
-            masks["nodes_encoder"] = _mlp_masks(ne, st["sv_ne"][1][0], N, False, ks)
-            masks["edges_encoder"] = to_caller(_mlp_masks(ee, st["sv_ee"][1][0], E, False, ks))
-            masks["decode_module"] = _mlp_masks(dec, st["sv_dec"][1][0], N, False, ks)
+            masks["nodes_encoder"] = _mlp_masks(ne, st["sv_ne"][1][0], N, False, ks, dev)
+            masks["edges_encoder"] = to_caller(_mlp_masks(ee, st["sv_ee"][1][0], E, False, ks, dev))
+            masks["decode_module"] = _mlp_masks(dec, st["sv_dec"][1][0], N, False, ks, dev)
             bspecs = plan.specs[3:]
         else:
             bspecs = plan.specs
         for b, sv in enumerate(st["svs"]):
             ke, kn, _ = sv[1]
-            masks[f"processor_list.{b}.edge_block"] = to_caller(_mlp_masks(bspecs[2 * b], ke[0], E, True, ks))
-            masks[f"processor_list.{b}.node_block"] = _mlp_masks(bspecs[2 * b + 1], kn[0], N, True, ks)
+            masks[f"processor_list.{b}.edge_block"] = to_caller(_mlp_masks(bspecs[2 * b], ke[0], E, True, ks, dev))
+            masks[f"processor_list.{b}.node_block"] = _mlp_masks(bspecs[2 * b + 1], kn[0], N, True, ks, dev)
         self.masks = masks
+
+
+class FlipStats(dict):
+    """A `record=` sink for the oracle's mlp that keeps flip statistics instead of the pre-activations
+    (graphs whose fp64 pre-activations would not fit: Cfg E, 1.4 GB per layer): per MLP layer, the count
+    of units whose pinned branch differs from the fp64 sign and their largest |z64| / mean |z64|. The
+    mlp appends its hidden layers' pre-activations in order (again when a checkpointed block is
+    recomputed: the layer index is the append count modulo the hidden layers)."""
+
+    def __init__(self, masks, hidden_layers=3):
+        super().__init__()
+        self._masks, self._nh, self._sinks = masks, hidden_layers, {}
+
+    def setdefault(self, prefix, default=None):
+        sink = self._sinks.get(prefix)
+        if sink is None:
+            stats = self
+
+            class _Sink:
+                count = 0
+
+                def append(self, z):
+                    i = self.count % stats._nh
+                    self.count += 1
+                    m = stats._masks[prefix][i]
+                    d = m != (z > 0)
+                    n = int(d.sum())
+                    if n:
+                        key = f"{prefix}.{2 * i}"
+                        r = float(z[d].abs().max() / z.abs().mean())
+                        old = dict.get(stats, key, {"flipped": 0, "max_rel_z": 0.0})
+                        dict.__setitem__(stats, key, {"flipped": max(old["flipped"], n),
+                                                      "max_rel_z": max(old["max_rel_z"], r)})
+
+            sink = self._sinks[prefix] = _Sink()
+        return sink
 
 
 def flips(masks, record):

@@ -296,7 +296,9 @@ def _aten_eval(ref, x, ei, ea, gy, mp, dtype, autocast=False):
     return out
 
 
-def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out):
+def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out, masks=None):
+    """masks (a tests/_masks.MaskRecorder): record the ReLU branch of every hidden unit libmgn took."""
+    from graphphysics.models import _engine
     from graphphysics.models.processors import EncodeProcessDecode
     from graphphysics.utils.data import Data
 
@@ -304,7 +306,11 @@ def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out):
     m = EncodeProcessDecode(mp, node_in, edge_in, out, h, compute_dtype=dtype).to(DEV)
     xd = x.to(DEV).detach().clone().requires_grad_(True)  # fresh leaves: never the fixture's tensors
     ed = ea.to(DEV).detach().clone().requires_grad_(True)
-    y = m(Data(x=xd, edge_index=ei, edge_attr=ed))
+    _engine.INSPECT = masks
+    try:
+        y = m(Data(x=xd, edge_index=ei, edge_attr=ed))
+    finally:
+        _engine.INSPECT = None
     (y * gy.to(DEV)).sum().backward()
     torch.cuda.synchronize()
     res = {"y": y.detach().double().cpu(), "x": xd.grad.double().cpu(), "e": ed.grad.double().cpu()}
@@ -314,8 +320,27 @@ def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out):
     return res
 
 
-def _rel(a, b):
-    return float((a - b).norm() / (b.norm() + 1e-300))
+def _pinned_eval(ref, x, ei, ea, gy, mp, masks, stats):
+    """_aten_eval in fp64 on libmgn's ReLU branch (tests/_masks.py; checkpointed blocks)."""
+    from torch.utils.checkpoint import checkpoint
+
+    p = {k: v.detach().to(DEV, torch.float64).requires_grad_(True) for k, v in ref.named_parameters()}
+    xd = x.to(DEV, torch.float64).requires_grad_(True)
+    ed = ea.to(DEV, torch.float64).requires_grad_(True)
+    kw = dict(masks=masks, record=stats)
+    xe = O.mlp(xd, p, "nodes_encoder", **kw)
+    e = O.mlp(ed, p, "edges_encoder", **kw)
+    for b in range(mp):
+        xe, e = checkpoint(O.graph_net_block, xe, ei, e, p, f"processor_list.{b}.", masks, stats, use_reentrant=False)
+    y = O.mlp(xe, p, "decode_module", norm=False, **kw)
+    keys = list(p)
+    grads = torch.autograd.grad((y * gy.to(DEV, torch.float64)).sum(), [xd, ed] + [p[k] for k in keys])
+    torch.cuda.synchronize()
+    out = {"y": y.detach().cpu(), "x": grads[0].cpu(), "e": grads[1].cpu()}
+    out.update({k: g.cpu() for k, g in zip(keys, grads[2:])})
+    del p, xd, ed, y, grads
+    torch.cuda.empty_cache()
+    return out
 
 
 @pytest.mark.parametrize("khop,mp,h", [(2, 15, 128), (1, 10, 64)])
@@ -323,13 +348,15 @@ def test_aneurysm_full_size_fp32_and_bf16_gradients(khop, mp, h):
     """Cfg E at full size: the 3D aneurysm graph with k-hop 2 (E = 1,395,256, in-degree up to 103) and
     the headline model (MP=15, h=128), and coarse-aneurysm.json's own sizes (k-hop 1, MP=10, h=64:
     training_config/coarse-aneurysm.json); inputs node_in 23, edge_in 4, out 3.
-      fp32: output rel-L2 <= 1e-4 vs the fp32 evaluation; output, every parameter gradient and the
-            input gradients (x, edge_attr) no further from fp64 than max(1e-3 [SURVEY §8c grads],
-            2 x the fp32 evaluation's own error).
+      fp32: output rel-L2 <= 1e-4 vs the fp32 evaluation; output (1e-5), every parameter gradient and
+            the input gradients (x, edge_attr) within SURVEY §8c's 1e-3 of the fp64 evaluation on
+            libmgn's ReLU branch (mask-pinned), every flipped unit a near-tie.
       bf16: output and every gradient no further from fp64 than 2 x the bf16 autocast evaluation's
             error (floor 1e-2), and the SAME on the rows of the highest in-degree nodes alone (nodes with
             in-degree >= the 99th percentile): an indexing error confined to long segments would stand out
             there while averaging away in the whole-tensor norm."""
+    from _masks import FlipStats, MaskRecorder
+
     n, ei, ea, x, y = _aneurysm(khop)
     g = torch.Generator().manual_seed(21)
     xin = torch.randn(n, 23, generator=g)
@@ -338,15 +365,30 @@ def test_aneurysm_full_size_fp32_and_bf16_gradients(khop, mp, h):
     ref = O.OracleEPD(mp, 23, 4, 3, h)
     r64 = _aten_eval(ref, xin, ei, ea.cpu(), gy.to(DEV, torch.float64), mp, torch.float64)
     r32 = _aten_eval(ref, xin, ei, ea.cpu(), gy.to(DEV), mp, torch.float32)
-    g32 = _libmgn_eval(xin, ei, ea, gy, mp, h, torch.float32, 23, 4, 3)
+    rec = MaskRecorder(device=DEV)
+    g32 = _libmgn_eval(xin, ei, ea, gy, mp, h, torch.float32, 23, 4, 3, masks=rec)
     assert _rel(g32["y"], r32["y"]) <= 1e-4
+    # fp32 gradients vs fp64 ON libmgn's ReLU branch (as tests/test_mask_pinned_gpu.py for Cfg B): 15
+    # blocks of 1.4M edges hold pre-activations within fp32 rounding of 0, which any fp32 summation order
+    # — PyTorch's atomics included — puts on either side of a ReLU, moving every upstream gradient by up
+    # to ~1e-3 (round 5: a reordered fp32 node-MLP GEMM moved block 12's edge W0 gradient to 1.07e-3 of
+    # the unpinned fp64 evaluation while PyTorch's own fp32 run sat at 2.5e-4 / 3.8e-4 in two runs).
+    # Pinned, what is left is rounding: every gradient within SURVEY §8(c)'s 1e-3, and every unit whose
+    # branch differs from the fp64 sign a near-tie (|z64| <= 1e-4 of its layer's mean |z|).
+    stats = FlipStats(rec.masks)
+    p64 = _pinned_eval(ref, xin, ei, ea, gy, mp, rec.masks, stats)
+    del rec
+    assert _rel(g32["y"], p64["y"]) <= 1e-5, _rel(g32["y"], p64["y"])
     worst = []
-    for k in r64:
-        e_got, e_ref = _rel(g32[k], r64[k]), _rel(r32[k], r64[k])
-        worst.append((e_got / max(1e-3, 2 * e_ref), k, e_got, e_ref))
-        assert e_got <= max(1e-3, 2 * e_ref), (k, e_got, e_ref)
-    print("\nfp32 worst (ratio, key, libmgn, aten-fp32):", sorted(worst)[-3:])
-    del g32, r32
+    for k in p64:
+        e_got, e_unpinned, e_ref = _rel(g32[k], p64[k]), _rel(g32[k], r64[k]), _rel(r32[k], r64[k])
+        worst.append((e_got, k, e_unpinned, e_ref))
+        assert e_got <= 1e-3, (k, e_got, e_unpinned, e_ref)
+    print("\nfp32 worst pinned (libmgn vs pinned fp64, key, vs unpinned fp64, aten-fp32 vs fp64):", sorted(worst)[-3:])
+    print("fp32 branch flips:", dict(stats))
+    for k, v in stats.items():
+        assert v["max_rel_z"] <= 1e-4, f"{k}: libmgn's branch differs from fp64 away from a tie: {v}"
+    del g32, r32, p64
     rac = _aten_eval(ref, xin, ei, ea.cpu(), gy.to(DEV), mp, torch.float32, autocast=True)
     gbf = _libmgn_eval(xin, ei, ea, gy, mp, h, torch.bfloat16, 23, 4, 3)
     deg = torch.bincount(ei[1].cpu(), minlength=n)

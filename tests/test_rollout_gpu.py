@@ -167,9 +167,26 @@ def test_inference_block_kernels_match_training_kernels():
     m = EncodeProcessDecode(15, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
     y_train = m(g)  # parameters require grad: training kernels with saves
     assert y_train.requires_grad
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(DEV)  # y_train's autograd graph holds the 15 blocks' saves
+    torch.cuda.reset_peak_memory_stats(DEV)
     with torch.no_grad():
         y_inf = m(g)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated(DEV) - base
     assert torch.equal(y_train.detach(), y_inf)
+    # no autograd graph -> no backward saves (round 5: needs_input_grad reports requires_grad even under
+    # torch.no_grad, so the grad mode is passed in): the no-grad forward's peak is one block's z / rden
+    # and the residual streams, a fraction of the training forward's R8 activations, masks and z
+    del y_inf
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(DEV)
+    base2 = torch.cuda.memory_allocated(DEV)
+    y_again = m(g)
+    torch.cuda.synchronize()
+    peak_train = torch.cuda.max_memory_allocated(DEV) - base2
+    del y_again
+    assert peak < 0.25 * peak_train, (peak, peak_train)
     from graphphysics import _native as nat
 
     d = m._get_plan().packed(DEV, nat.MGN_BF16).descs
