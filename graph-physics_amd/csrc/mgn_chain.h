@@ -23,6 +23,27 @@ struct ChainFwdArgs {
     int64_t mask_stride;        // 64-bit words per layer
 };
 
+// Edge MLP weight gradients of layers 1..3 with their inputs RECOMPUTED (round 5): the forward writes no
+// R8 activations (chain16_fwd_kernel SACT = false); one workgroup per row chunk re-runs layers 0..2 on
+// its rows (the forward's exact operations: bit-identical X1..X3) and accumulates dW_l = dZ_lᵀ X_l,
+// db_l = Σ dZ_l from the backward's R8 dZ saves, into its slab.
+struct ChainRewArgs {
+    const __bf16* e;            // [M][128] the block's edge state (target-sorted)
+    const __bf16* proj;         // [N][256] its node projections (pair layout, b0 folded in P_i)
+    const int32_t* proj_i;
+    const int32_t* proj_j;
+    const __bf16* wpack;        // forward fragments (layers 0..2 used)
+    int64_t woff[4];
+    int32_t wks[4];
+    const float* bias[4];
+    const __bf16* dz8;          // R8 [4][RP][128] dZ saves of the edge backward (layers 1..3 used)
+    int64_t M, RP;
+    int32_t rows_per_chunk, nchunks;
+    float* part;                // slab c at part + c * G
+    int64_t G;
+    int64_t w_off[4], b_off[4]; // layer l's weight / bias offsets in a slab
+};
+
 struct ChainBwdArgs {
     const __bf16* dout;         // [M][128] de_out
     const __bf16* gath;         // [N][128] d_aggr, added at gath_idx[row]
@@ -109,8 +130,15 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
 // nparts: number of dscale partial rows written (the reduction's row count)
 // Pair layout (mgn_chain16.hip col_of): the bf16 node projections P are always in it; z_p2 / p2 =
 // the block's node MLP is chained too (then the edge z and d_aggr rows are in it as well)
+// save_act = false (the recomputed weight gradients, chain16_edge_wgrad_recompute): ReLU masks, z and rden
+// only — no R8 layer inputs
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2);
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act = true);
+// dW / db of the edge MLP's layers 1..3 into slabs part[0 .. nchunks) (chunks of rows_per_chunk rows, a
+// multiple of 32), their inputs recomputed from e and the projections (ChainRewArgs)
+int chain16_edge_wgrad_recompute(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
+                                 int64_t M, const void* dz8, float* part, int64_t G, int rows_per_chunk, int nchunks,
+                                 hipStream_t st);
 // din2 / dout2 (p2 only): de_out read / de written in the pair layout (between the edge backwards of
 // consecutive processor blocks, mgn_block_backward_deferred2)
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,

@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "mgn_chain.h"
+#include "mgn_chain16_dev.h"
 
 // Diagnostics builds only (-DMGN_ABLATE=bits, results wrong when nonzero; see mgn_mlp.hip): edge
 // forward 1 = P gathers from row 0 (cache-resident), 2 = no P loads, 4 = no weight-staging loads,
@@ -46,13 +47,6 @@
 
 namespace {
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-constexpr int H = 128;
-constexpr int TR = 16;                 // edges per wave tile
-constexpr int NW = 8;                  // waves per workgroup (2 per SIMD)
-constexpr int FRAG = 512;              // bf16 per 16x16x32 operand fragment (64 lanes x 8)
-constexpr int LFR = 32;                // fragments per layer: 8 out-tiles x 4 k-steps
 constexpr int SLD = H + 8;             // scratch row stride (bf16)
 constexpr int SROWS = 8;               // scratch rows (one R8 octet per pass)
 constexpr size_t LDS_W = (size_t)4 * LFR * FRAG * 2;   // 128 KiB
@@ -108,19 +102,11 @@ __device__ unsigned long long g_wave_t[4][4096][2];
 #define WAVE_REC(k)
 #endif
 
-__device__ __forceinline__ f4 mfma16(const bf16x8& a, const bf16x8& b, const f4& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 
-__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 template <class T>
 __device__ __forceinline__ void pin(const T& v) { asm volatile("" ::"v"(v)); }
 
-__device__ __forceinline__ f4 bf4(u32x2 v) {
-    const bf16x4 b = __builtin_bit_cast(bf16x4, v);
-    return f4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
-}
 
 // the 4 components of v summed over the 16 lanes of a DPP row, transposing as it goes: lane m
 // returns the total of component 2(m&1) + ((m>>1)&1) (pairs m^1 trade two components, pairs m^2
@@ -166,71 +152,6 @@ __device__ __forceinline__ void relu_mask(f4 (&acc)[8], unsigned w) {
     relu_mask_seq(acc, w, std::make_integer_sequence<int, 32>{});
 }
 
-// Weight image: fragment (l, t, s) lane (r, g) element j = A_l[16t + r][32s + 16(j>>2) + 4g + (j&3)]
-// (A = W forward, Wᵀ backward). Linear walk over libmgn's 16x16x32 packs (16-byte coalesced loads):
-// a source chunk holds 8 consecutive reduction indices 32s + 8q .. +7 of one row; its halves go to
-// lane groups g = 2(q&1) + half, element group jg = q>>1.
-template <int NL = 4, int NT = NW * 64>
-__device__ __forceinline__ void stage16(__bf16* W, const __bf16* pack, const int64_t* woff, const int* wks,
-                                        bool transposed, int tid = -1) {
-    constexpr int TOT = NL * 2048, PER = (TOT + NT - 1) / NT;  // 16 chunks per thread (4 layers, 512 threads)
-    if (tid < 0) tid = threadIdx.x;
-    u32x4 v[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int it = tid + u * NT;
-        if (TOT % NT != 0 && it >= TOT) break;
-        const int l = it >> 11, c = it & 2047;
-        const int tile = c >> 6, lane16 = c & 63;
-        const int rt = tile >> 2, ks = tile & 3;
-        const int ksl = transposed ? 4 : wks[l];
-        if (MGN_ABLATE & 4) {
-            v[u] = u32x4{0u, 0u, 0u, 0u};
-            continue;
-        }
-        v[u] = *reinterpret_cast<const u32x4*>(pack + woff[l] + ((int64_t)(rt * ksl + ks) * 64 + lane16) * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int it = tid + u * NT;
-        if (TOT % NT != 0 && it >= TOT) break;
-        const int l = it >> 11, c = it & 2047;
-        const int tile = c >> 6, lane16 = c & 63;
-        const int rt = tile >> 2, ks = tile & 3;
-        const int r = lane16 & 15, q = lane16 >> 4;
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int g = (2 * q + half) & 3, jg = q >> 1;
-            const u32x2 w = {v[u][2 * half], v[u][2 * half + 1]};
-            *reinterpret_cast<u32x2*>(W + ((size_t)((l * 8 + rt) * 4 + ks) * 64 + r + 16 * g) * 8 + jg * 4) = w;
-        }
-    }
-}
-
-__device__ __forceinline__ bf16x8 wfrag(const __bf16* W, int l, int t, int s, int lane) {
-    return *reinterpret_cast<const bf16x8*>(W + ((size_t)((l * 8 + t) * 4 + s) * 64 + lane) * 8);
-}
-
-// acc = bias (LDS vector, features 16t + 4g..; nullptr: 0) + W_l · B: the bias rides in the MFMA
-// accumulator instead of one v_add per output element after it
-__device__ __forceinline__ void acc_init(f4 (&acc)[8], const float* bias, int lane) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-        acc[t] = bias ? *reinterpret_cast<const f4*>(bias + 16 * t + 4 * (lane >> 4)) : f4{0.f, 0.f, 0.f, 0.f};
-}
-
-__device__ __forceinline__ void gemm16(f4 (&acc)[8], const __bf16* W, int l, const bf16x8 (&B)[4], int lane,
-                                       const float* bias = nullptr) {
-    acc_init(acc, bias, lane);
-    // one k-step's 8 fragments in flight at a time (the other wave on the SIMD covers the LDS
-    // latency); without the fence the scheduler hoists all 32 reads and the backward spills
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] = mfma16(wfrag(W, l, t, s, lane), B[s], acc[t]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
 
 // One layer's GEMM that also stores its B operand (= the layer's input, bf16) as R8 octets and/or
 // row-major rows through the wave's 8-row scratch, with the LDS round trips placed between the
@@ -312,30 +233,7 @@ __device__ __forceinline__ void gemm16_st(f4 (&acc)[8], const __bf16* W, int l, 
     lds_fence();  // scratch free for the next user
 }
 
-__device__ __forceinline__ void to_operand(const f4 (&v)[8], bf16x8 (&B)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) B[s][j] = (__bf16)v[2 * s + (j >> 2)][j & 3];
-}
 
-// Pair layout (P2) of a bf16 row of 128 features, for rows this library both writes and gathers
-// back in the accumulator layout (node projections P, the edge MLP's z, the node MLP's z, d_aggr):
-// feature 16t + 4g + r sits at 32(t>>1) + 8g + 4(t&1) + r, so the two quads of lane group g for the
-// tile pair (2i, 2i+1) are one 16-byte load (4 loads of 16 B per row and lane instead of 8 of 8 B).
-template <bool P2>
-__device__ __forceinline__ int col_of(int t, int g) {
-    return P2 ? 32 * (t >> 1) + 8 * g + 4 * (t & 1) : 16 * t + 4 * g;
-}
-// the 8 accumulator-layout quads (features 16t + 4g .. +3) of a P2 row
-__device__ __forceinline__ void load_p2(u32x2 (&o)[8], const __bf16* row, int g) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(row + 32 * i + 8 * g);
-        o[2 * i] = u32x2{w[0], w[1]};
-        o[2 * i + 1] = u32x2{w[2], w[3]};
-    }
-}
 
 // write this lane's 32 values of row m (&7) of one octet into the scratch (P2: pair layout)
 template <bool P2 = false>
@@ -432,16 +330,6 @@ static_assert((MGN_EDGE_WAVES == 8 || MGN_EDGE_WAVES == 12) && (MGN_EDGE_BWD_WAV
 constexpr int edge_waves() { return MGN_EDGE_WAVES; }
 constexpr int edge_bwd_waves() { return MGN_EDGE_BWD_WAVES; }
 
-void layer_offsets(const mgn_mlp* m, int64_t* woff, int* wks) {
-    int64_t o = 0;
-    for (int l = 0; l < 4; ++l) {
-        int n, k;
-        mlp_layer_shape(*m, l, &n, &k);
-        woff[l] = o;
-        wks[l] = cdiv(k, 32);
-        o += linear_pack_elems(n, k, MGN_BF16);
-    }
-}
 
 // ------------------------------------------------------------------------------------ forward
 struct In16 {
@@ -470,7 +358,9 @@ __device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, in
 // written — no R8 layer inputs, no ReLU masks (≈ 40 % of the training forward's HBM bytes).
 // P is in the pair layout; ZP2: z too (the chained node MLP and the chained backward read it so;
 // false: row-major, for a generic node MLP)
-template <bool SAVE, int NWK, bool ZP2>
+// SACT = false (with SAVE): ReLU masks, z, rden but no R8 layer inputs (their weight gradients recompute
+// them: chain16_rew_kernel)
+template <bool SAVE, int NWK, bool ZP2, bool SACT = true>
 __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -518,7 +408,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         for (int l = 0; l < 3; ++l) {
             if (l == 0)
                 gemm16(acc, W, 0, in.eb, lane);
-            else if (SAVE)
+            else if (SAVE && SACT)
                 gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.act8 + a.act_off[l], nullptr}, tile, a.M, vec + l * H);
             else
                 gemm16(acc, W, l, B, lane, vec + l * H);
@@ -540,7 +430,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
             STAMP(3);
         }
         // layer 3 (stores its input, the R8 save of layer 3) + RMSNorm + residual
-        if (SAVE)
+        if (SAVE && SACT)
             gemm16_st(acc, W, 3, B, lane, scr, StoreDst{a.act8 + a.act_off[3], nullptr}, tile, a.M, vec + 3 * H);
         else
             gemm16(acc, W, 3, B, lane, vec + 3 * H);
@@ -1639,25 +1529,10 @@ __global__ __launch_bounds__(NW * 64) void chain16_dense_bwd_kernel(ChainDenseBw
     }
 }
 
-int set_lds_once(const void* fn, size_t bytes) {
-    static std::mutex mu;
-    static const void* done[32] = {};
-    std::lock_guard<std::mutex> lk(mu);
-    for (const void* d : done)
-        if (d == fn) return 0;
-    MGN_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-    for (const void*& d : done)
-        if (!d) {
-            d = fn;
-            break;
-        }
-    return 0;
-}
-
 }  // namespace
 
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2) {
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act) {
     ChainFwdArgs a;
     memset(&a, 0, sizeof(a));
     a.e = reinterpret_cast<const __bf16*>(e);
@@ -1682,12 +1557,15 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
     const int nwk = edge_waves();
     // inference (no saves) always feeds the chained node MLP: z in the pair layout
     MGN_REQUIRE(sv->act || z_p2, "chained inference edge forward: z must be in the pair layout");
-    const auto kern = nwk == 12 ? (!sv->act ? chain16_fwd_kernel<false, 12, true>
-                                   : z_p2   ? chain16_fwd_kernel<true, 12, true>
-                                            : chain16_fwd_kernel<true, 12, false>)
-                                : (!sv->act ? chain16_fwd_kernel<false, 8, true>
-                                   : z_p2   ? chain16_fwd_kernel<true, 8, true>
-                                            : chain16_fwd_kernel<true, 8, false>);
+    MGN_REQUIRE(save_act || (sv->act && z_p2), "edge forward without R8 saves: the chained block path only");
+    const auto kern = nwk == 12 ? (!sv->act   ? chain16_fwd_kernel<false, 12, true>
+                                   : !save_act ? chain16_fwd_kernel<true, 12, true, false>
+                                   : z_p2      ? chain16_fwd_kernel<true, 12, true>
+                                               : chain16_fwd_kernel<true, 12, false>)
+                                : (!sv->act   ? chain16_fwd_kernel<false, 8, true>
+                                   : !save_act ? chain16_fwd_kernel<true, 8, true, false>
+                                   : z_p2      ? chain16_fwd_kernel<true, 8, true>
+                                               : chain16_fwd_kernel<true, 8, false>);
     const size_t lds = lds_fwd(nwk);
     if (int e2 = set_lds_once((const void*)kern, lds)) return e2;
     ProfScope ps(PROF_FWD_EDGE, st);

@@ -16,6 +16,7 @@
 // Backward = data-gradient chain per tile (same structure, transposed weight fragments) +
 // weight-gradient GEMMs over row chunks (K = rows) with a fixed-order partial-slab reduction.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -1634,9 +1635,14 @@ struct RedDesc {
     // optional column region of W0 ([w0_n][w0_k] at the start of the slab rows): columns >= xcol0
     // sum only their first nchunks_x slabs (w0_k == 0: none)
     int32_t w0_n, w0_k, xcol0, nchunks_x;
+    // optional tail [hoff, G) summed over its own first nchunks_h slabs (the recomputed edge
+    // weight gradients of layers 1.., chain16_edge_wgrad_recompute; hoff == 0: none)
+    int64_t hoff;
+    int32_t nchunks_h, pad;
 };
 // slabs summed for output g
 __device__ __forceinline__ int red_nchunks(const RedDesc& d, int64_t g) {
+    if (d.hoff > 0 && g >= d.hoff) return d.nchunks_h;
     if (d.w0_k > 0 && g < (int64_t)d.w0_n * d.w0_k && (int)(g % d.w0_k) >= d.xcol0) return d.nchunks_x;
     return d.nchunks;
 }
@@ -2289,6 +2295,7 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
     const int64_t tile = (int64_t)blockIdx.x * F32N_WAVES + (threadIdx.x >> 6);
     const int64_t row = tile * 16 + ri;
     const bool valid = row < a.M;
+    F32C_STAMP_DECL;
     const float* pk = reinterpret_cast<const float*>(a.wpack);
     // layer 0's two images land during phase A
     f32n_stage(pk + chain_image_off(H, 2 * H, 0), img0);
@@ -2340,8 +2347,10 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) st4(reinterpret_cast<float*>(a.agg_save) + row * H + 16 * t + 4 * g, ag[t]);
     }
+    F32C_STAMP(5);  // phase A issued and consumed (x rows, aggregation)
     f32c_stage_wait();
     __syncthreads();
+    F32C_STAMP(0);
     f4 acc[8], x1[8];
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) acc[nt] = *reinterpret_cast<const f4*>(vec + 16 * nt + 4 * g);
@@ -2351,12 +2360,15 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
     f32n_stage(nxt, img0);           // layer 1's image streams in under the aggregate block
     pk += linear_pack_elems(H, H, MGN_F32);
     f32c_gemm(acc, ag, img1, lane);  // aggr block
+    F32C_STAMP(1);
     float* act = reinterpret_cast<float*>(a.act8);
     const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
     unsigned long long word = f32c_relu(x1, acc, lane);
     if (lane < 32) a.mask[tile * 32 + lane] = word;
+    F32C_STAMP(2);
     f32c_stage_wait();
     __syncthreads();
+    F32C_STAMP(3);
     // layers 1..3 (layer l on buffer (l + 1) & 1): layer l+1's image streams into the other buffer
 #pragma unroll 1
     for (int l = 1; l < 4; ++l) {
@@ -2369,11 +2381,14 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
         for (int nt = 0; nt < 8; ++nt) acc[nt] = *reinterpret_cast<const f4*>(vec + l * H + 16 * nt + 4 * g);
         float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
         f32c_gemm(acc, x1, cur, lane, sv + r8);  // its input's R8 save, under the MFMAs
+        F32C_STAMP(1);
         if (l < 3) {
             word = f32c_relu(x1, acc, lane);
             if (lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
+            F32C_STAMP(2);
             f32c_stage_wait();
             __syncthreads();
+            F32C_STAMP(3);
         }
     }
     // last Linear (bias in the accumulator): RMSNorm, residual x
@@ -2401,6 +2416,8 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
             }
         }
     }
+    F32C_STAMP(4);
+    F32C_STAMP_PRINT("f32nf");
 }
 
 __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
@@ -2413,6 +2430,7 @@ __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
     const int64_t tile = (int64_t)blockIdx.x * F32N_WAVES + wave;
     const int64_t row = tile * 16 + ri;
     const bool valid = row < a.M;
+    F32C_STAMP_DECL;
     const float* wt = reinterpret_cast<const float*>(a.wtpack);
     const int64_t off1 = linear_pack_elems(H, 2 * H, MGN_F32);       // transposed pack offsets
     const int64_t off2 = off1 + linear_pack_elems(H, H, MGN_F32), off3 = off2 + linear_pack_elems(H, H, MGN_F32);
@@ -2471,8 +2489,10 @@ __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
         const float dsum = f32c_row16_sum4(dsc, ri);
         if (ri < 4) red[wave * H + 16 * nt + 4 * g + r4] = dsum;
     }
+    F32C_STAMP(5);
     f32c_stage_wait();
     __syncthreads();
+    F32C_STAMP(0);
     float* dz8 = reinterpret_cast<float*>(a.dz8);
     const int64_t r8 = f32c_r8t(row, g);
     if (!(wave & 1) && ri == 0) {  // partials per 32 rows (the generic node kernel's count)
@@ -2501,6 +2521,7 @@ __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
         const int l = 3 - i;  // dZ_l feeds this GEMM (i = 4: dZ0 again, the aggr block)
         float* sv = i < 4 ? dz8 + (int64_t)l * a.RP * H + r8 : nullptr;
         f32c_gemm(acc, dz, cur, lane, sv);
+        F32C_STAMP(1);
         if (i < 3) {
             const unsigned long long mine = l == 3 ? mw[2] : l == 2 ? mw[1] : mw[0];
 #pragma unroll
@@ -2520,11 +2541,14 @@ __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
 #pragma unroll
             for (int nt = 0; nt < 8; ++nt) st4(reinterpret_cast<float*>(a.o2) + row * H + 16 * nt + 4 * g, acc[nt]);
         }
+        F32C_STAMP(2);
         if (i < 4) {
             f32c_stage_wait();
             __syncthreads();
         }
+        F32C_STAMP(3);
     }
+    F32C_STAMP_PRINT("f32nb");
 }
 
 // --------------------------------------------------------------------------- host side
@@ -2850,6 +2874,28 @@ int64_t wgrad_max_chunks(int64_t RP, int H = 128) {
     return c < 1 ? 1 : c;
 }
 int wgrad_wgs_per_cu(int H) { return H <= 32 ? MGN_WG_PER_CU32 : 1; }
+// Slabs of the recomputed edge weight gradients (chain16_edge_wgrad_recompute: one 8-wave workgroup
+// per CU, layers 1..3 regions only): up to MGN_REW_CHUNKS (env, default MGN_REW_MAXCH) chunks of at
+// least 256 rows. The bf16 h=128 slab buffers (keep_layout, mlp_bwd_ws) hold max(this, wgrad_max_chunks).
+#ifndef MGN_REW_MAXCH
+#define MGN_REW_MAXCH 256
+#endif
+int64_t rew_max_chunks(int64_t RP) {
+    static const int64_t cap = [] {
+        const char* v = getenv("MGN_REW_CHUNKS");
+        const long c = v ? atol(v) : MGN_REW_MAXCH;
+        return (int64_t)(c < 1 ? 1 : c > 1024 ? 1024 : c);
+    }();
+    int64_t c = RP / 256;
+    if (c > cap) c = cap;
+    return c < 1 ? 1 : c;
+}
+int64_t slab_chunks(int64_t RP, const mgn_mlp* m) {
+    const int64_t c = wgrad_max_chunks(RP, m->hidden);
+    if (m->hidden != 128 || m->dtype != MGN_BF16) return c;
+    const int64_t r = rew_max_chunks(RP);
+    return r > c ? r : c;
+}
 int wgrad_rows_per_chunk(int64_t RP, int njobs, int H = 128) {
     int64_t chunks = (int64_t)wgrad_wgs_per_cu(H) * wgrad_cus() / njobs;
     const int64_t cap = wgrad_max_chunks(RP, H);
@@ -2873,6 +2919,9 @@ RedDesc red_desc(const mgn_mlp* m, const float* part, int nchunks, const float* 
     d.NS = m->has_norm ? m->out_dim : 0;
     d.w0_n = d.w0_k = d.xcol0 = 0;
     d.nchunks_x = nchunks;
+    d.hoff = 0;
+    d.nchunks_h = nchunks;
+    d.pad = 0;
     const bool vec = (d.G & 3) == 0 && ((uintptr_t)part & 15) == 0;
     d.blocks = (int32_t)(cdiv64(d.G, vec ? 256 : 64) + d.NS);  // = red_gblocks + NS
     return d;
@@ -3119,6 +3168,10 @@ struct BlockWgradIn {
     const float* ndsp;
     int nntiles;
     float *npart, *ngrads;
+    // chained bf16, non-NULL: the edge layers 1..3 weight gradients from inputs recomputed out of e
+    // and the forward's node projections (mgn_block_saved.proj; pi / pj the P_i / P_j gather indices)
+    const void* proj;
+    const int32_t *pi, *pj;
 };
 
 // T = __bf16: the chained bf16 blocks (dZ0 row-major, the bf16 ring); T = float: fp32 h=128 blocks on
@@ -3145,14 +3198,28 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     // edge slab buffer holds wgrad_max_chunks(RPE) slabs (keep_layout, mlp_bwd_ws): cp is capped
     // there (graphs with more nodes than edges).
     const int cus = wgrad_cus();
+    // recomputed edge layers 1..3 (chain16_edge_wgrad_recompute): their own launch ahead of the ring,
+    // cr chunks of 32-row steps over the first cr edge slabs; the ring keeps one edge job (W0's e block)
+    const bool rew = !F32 && in.proj != nullptr;
+    const int ejobs = rew ? 1 : 4;
+    int cr = 0;
+    if (rew) {
+        int64_t c = rew_max_chunks(RPE);
+        if (c > cus) c = cus;
+        const int64_t rr = cdiv64(cdiv64(RPE, c), 32) * 32;
+        cr = (int)cdiv64(RPE, rr);
+        if (int e2 = chain16_edge_wgrad_recompute(edge, in.e, in.proj, in.pi, in.pj, in.E, in.edz8, in.epart,
+                                                  grad_G(edge), (int)rr, cr, st))
+            return e2;
+    }
     int ce = 1, cn = 1, cp = 1;
     int re = 0, rn = 0, rp = 0;
     {
-        const int64_t total = 4 * RPE + 7 * RPN;
+        const int64_t total = ejobs * RPE + 7 * RPN;
         for (int64_t target = cdiv64(cdiv64(total, cus), 64) * 64;; target += 64) {
             re = rows_for(RPE, target, &ce);
             rn = rows_for(RPN, target, &cn);
-            if (4 * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
+            if (ejobs * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
         }
         const int64_t cpmax = wgrad_max_chunks(RPE);
         const int64_t c = cn < cpmax ? cn : cpmax;
@@ -3189,6 +3256,7 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     const int64_t Ge = grad_G(edge), Gn = grad_G(node);
     // edge MLP over edge rows (heaviest first: dispatch order)
     int64_t off = 0;
+    int64_t hoff = 0;
     for (int l = 0; l < edge->n_layers; ++l) {
         int n, k;
         mlp_layer_shape(*edge, l, &n, &k);
@@ -3197,7 +3265,8 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
             add(F32 ? (const void*)z : in.dz0, in.e, H, RPE, in.E, in.epart, Ge, off, off + (int64_t)n * k, n, k, k, 0,
                 re, ce);
             r.job[nj - 1].zrm = F32 ? 0 : 1;
-        } else
+            hoff = off + (int64_t)n * k + n;
+        } else if (!rew)
             add(z, reinterpret_cast<const T*>(in.eact) + act_off(*edge, in.E, l, 1), 0, RPE, in.E, in.epart, Ge,
                 off, off + (int64_t)n * k, n, k, act_cols(*edge, l), 0, re, ce);
         off += (int64_t)n * k + n;
@@ -3230,6 +3299,10 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     d[0].w0_k = edge->in_dim;
     d[0].xcol0 = H;
     d[0].nchunks_x = cp;
+    if (rew) {  // layers 1..3 of the edge slabs: the recomputed launch's cr chunks
+        d[0].hoff = hoff;
+        d[0].nchunks_h = cr;
+    }
     (void)re;
     if (defer) {  // the caller reduces later (mgn_wgrad_reduce_many): slabs + partials must persist
         defer[0] = d[0];
@@ -3369,7 +3442,7 @@ size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
     // dscale partial rows: the most any backward kernel writes (generic: one per 32-row tile;
     // chained node kernel: one per workgroup, at most one per 16-row tile)
     const int64_t ntiles = rows_pad(M) / 16;
-    const int64_t nchunks = wgrad_max_chunks(rows_pad(M), m->hidden);
+    const int64_t nchunks = slab_chunks(rows_pad(M), m);
     size_t b = align_up((size_t)m->n_layers * rows_pad(M) * m->hidden * es);  // dz8
     b += align_up((size_t)ntiles * m->out_dim * sizeof(float));              // dscale partials
     b += align_up((size_t)nchunks * grad_G(m) * sizeof(float));              // wgrad partial slabs
@@ -3972,6 +4045,12 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
                 "inference block forward (saved act = NULL) needs the chained bf16 h=128 path "
                 "(mgn_block_forward_inference_supported)");
     MGN_REQUIRE(ws_bytes >= block_fwd_ws(t, edge) && (ws || t->num_nodes == 0), "block forward workspace too small");
+    // saved->proj (ABI v16): no R8 saves of the edge MLP's hidden-layer inputs, the backward recomputes
+    // them from e and the projections this call leaves in ws
+    const bool rew = saved->proj != nullptr;
+    MGN_REQUIRE(!rew || (!infer && chain_eligible(edge) && chain_node_eligible(node) && saved->proj == ws &&
+                         t->num_nodes > 0 && t->num_edges > 0),
+                "saved->proj: a training forward of chained bf16 h=128 edge and node MLPs, proj == ws");
     hipStream_t st = (hipStream_t)stream;
     const int dt = edge->dtype;
     float* proj = reinterpret_cast<float*>(ws);
@@ -4010,7 +4089,7 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     }
     if (chain) {
         if (int r = chain16_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st,
-                                         chain_node_eligible(node)))
+                                         chain_node_eligible(node), !rew))
             return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
                                    nullptr, nullptr, st)) {
@@ -4133,7 +4212,7 @@ static KeepLayout keep_layout(const mgn_topology* t, const mgn_mlp* edge, const 
     k.edsp = o;
     o += align_up((size_t)(RPE / 16) * edge->out_dim * sizeof(float));
     k.epart = o;
-    o += align_up((size_t)wgrad_max_chunks(RPE, edge->hidden) * grad_G(edge) * sizeof(float));
+    o += align_up((size_t)slab_chunks(RPE, edge) * grad_G(edge) * sizeof(float));
     k.ndsp = o;
     o += align_up((size_t)(RPN / 16) * node->out_dim * sizeof(float));
     k.npart = o;
@@ -4317,6 +4396,9 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         in.nntiles = chain16_node_backward_parts(N);
         in.npart = c.npart;
         in.ngrads = node_grads;
+        in.proj = saved->proj;
+        in.pi = t->csc_dst;
+        in.pj = t->csc_src;
         return block_wgrad_ring<__bf16>(edge, node, in, st, keep ? defer : nullptr);
     }
     if (c.ring32 || c.gen1) {
@@ -4340,6 +4422,8 @@ static int block_backward_wgrad_impl(const mgn_topology* t, const mgn_mlp* edge,
         in.nntiles = (int)(rows_pad(N) / bm_host(dt, MODE_NODE));
         in.npart = c.npart;
         in.ngrads = node_grads;
+        in.proj = nullptr;
+        in.pi = in.pj = nullptr;
         if (c.ring32) return block_wgrad_ring<float>(edge, node, in, st, keep ? defer : nullptr);
         int rc = 0;
         if (dt == MGN_F32) {

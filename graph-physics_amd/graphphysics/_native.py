@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 15  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 16  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -47,12 +47,13 @@ class MlpSaved(ctypes.Structure):
 
 
 class BlockSaved(ctypes.Structure):
-    _fields_ = [("edge", MlpSaved), ("node", MlpSaved), ("aggr", _vp)]
+    _fields_ = [("edge", MlpSaved), ("node", MlpSaved), ("aggr", _vp), ("proj", _vp)]
 
 
 class WgradReduce(ctypes.Structure):
     _fields_ = [("part", _vp), ("dsp", _vp), ("grads", _vp), ("G", _i64), ("nchunks", _i32), ("ntiles", _i32),
-                ("NS", _i32), ("blocks", _i32), ("w0_n", _i32), ("w0_k", _i32), ("xcol0", _i32), ("nchunks_x", _i32)]
+                ("NS", _i32), ("blocks", _i32), ("w0_n", _i32), ("w0_k", _i32), ("xcol0", _i32), ("nchunks_x", _i32),
+                ("hoff", _i64), ("nchunks_h", _i32), ("pad", _i32)]
 
 
 class NormalizerState(ctypes.Structure):

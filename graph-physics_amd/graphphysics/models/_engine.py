@@ -79,6 +79,16 @@ def _grad_ready(G, lo, hi):
 # processor blocks hand the next block's node projections over from their node-MLP kernel
 # (mgn_block_forward_chain); False: every block launches its own projection kernel (tests compare)
 CHAIN_PROJ = True
+# chained bf16 h=128 processor blocks in training: the edge MLP's hidden-layer inputs are not saved by
+# the forward; the backward's weight gradients recompute them from e and the block's node projections,
+# which stay in a per-block forward workspace (mgn_block_saved.proj, ABI v16; bit-identical inputs, the
+# weight-gradient sums in another order). MGN_REW: "auto" (default) for graphs of at least
+# REW_MIN_EDGES edges, "1" always, "0" never. Measured (profiles/r05_rew_ab.txt): the saves of a
+# cylinder batch-8 block (95k edges, 73 MB) stay in the 256 MB Infinity Cache and cost the forward
+# 6 µs, less than the recomputation (-8 % steps/s with it); an aneurysm block's (1.4M edges, 1.1 GB)
+# go to HBM and cost 230 µs (+6.6 % steps/s with it)
+REW = os.environ.get("MGN_REW", "auto")
+REW_MIN_EDGES = 1 << 18
 # processor blocks' weight-gradient reductions deferred to one launch after the last block
 # (mgn_block_backward_deferred + mgn_wgrad_reduce_many); False: one reduction per block (same sums)
 DEFER_REDUCE = True
@@ -456,8 +466,13 @@ def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
     return s, (act, mask, z, rden)
 
 
-def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device):
+def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device, edge_act=True):
+    """edge_act False (mgn_block_saved.proj): the edge MLP's R8 inputs are never written — a
+    one-element placeholder (non-NULL: the training forward's kernels)."""
     se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True, True)
+    if not edge_act:
+        ke = (_empty(1, tdt, device),) + tuple(ke[1:])
+        se.act = ke[0].data_ptr()
     sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None, True)
     aggr = _empty(topo.num_nodes * espec.width, tdt, device)
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
@@ -586,9 +601,12 @@ class EPDFunction(torch.autograd.Function):
         nb = len(bspecs) // 2
         scratch = None
         # node projections hand-off: block b's node kernel writes block b+1's P into the other of two
-        # workspaces (mgn_block_forward_chain), so blocks after the first launch no projection kernel
-        fwss = [_fwd_ws_block(topo, bdescs[0], bdescs[1], dev), _fwd_ws_block(topo, bdescs[0], bdescs[1], dev)] \
-            if nb else None
+        # workspaces (mgn_block_forward_chain), so blocks after the first launch no projection kernel.
+        # rew: one workspace per block, kept for the backward (mgn_block_saved.proj)
+        rew = train and (REW == "1" or (REW == "auto" and E >= REW_MIN_EDGES)) and nb > 0 and N > 0 and E > 0 and all(
+            nat.lib().mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
+            for b in range(nb))
+        fwss = [_fwd_ws_block(topo, bdescs[0], bdescs[1], dev) for _ in range(nb if rew else 2)] if nb else None
         ready = ctypes.c_int32(0)
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
@@ -597,14 +615,18 @@ class EPDFunction(torch.autograd.Function):
                         ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1])):
                     sv = _alloc_block_infer(es_, topo, tdt, dev)  # no backward saves
                 else:
-                    sv = _alloc_block_saved(bdescs[2 * b], bdescs[2 * b + 1], es_, ns_, topo, tdt, dev)
+                    sv = _alloc_block_saved(bdescs[2 * b], bdescs[2 * b + 1], es_, ns_, topo, tdt, dev,
+                                            edge_act=not rew)
                 if not train:
                     scratch = sv
             else:
                 sv = scratch
             x1 = torch.empty((N, H), dtype=tdt, device=dev)
             e1 = torch.empty((E, H), dtype=tdt, device=dev)
-            fws, nws = fwss[b % 2], fwss[(b + 1) % 2]
+            fws, nws = (fwss[b], fwss[min(b + 1, nb - 1)]) if rew else (fwss[b % 2], fwss[(b + 1) % 2])
+            if rew:
+                sv[0].proj = fws.data_ptr()
+                sv = (sv[0], sv[1] + (fws,))
             nxt = ctypes.byref(bdescs[2 * b + 2]) if CHAIN_PROJ and b + 1 < nb else None
             proj_ready = ready.value
             nat.check(nat.lib().mgn_block_forward_chain(

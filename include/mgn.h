@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 15
+#define MGN_ABI_VERSION 16
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -178,6 +178,12 @@ typedef struct mgn_block_saved {
     mgn_mlp_saved edge; /* rows = E (target-sorted order) */
     mgn_mlp_saved node; /* rows = N */
     void* aggr;         /* [N, hidden] aggregated messages (dtype) */
+    /* ABI v16: NULL, or (training forward of a chained bf16 h=128 block) the block's forward workspace
+     * `ws`, which the caller then keeps intact until the block's backward: the forward writes no R8
+     * inputs of the edge MLP's hidden layers (edge.act is not written) and the backward recomputes them
+     * from e and the node projections in ws for those layers' weight gradients (one pass, no re-read
+     * of saved activations). */
+    void* proj;
 } mgn_block_saved;
 
 /* x:[N,h], e:[E,h] (target-sorted edge order), dtype of the MLPs. x_out/e_out may not alias.
@@ -234,6 +240,8 @@ typedef struct mgn_wgrad_reduce {
     int64_t G;
     int32_t nchunks, ntiles, NS, blocks;
     int32_t w0_n, w0_k, xcol0, nchunks_x; /* W0 columns >= xcol0 sum only nchunks_x slabs */
+    int64_t hoff;                         /* ABI v16: outputs g >= hoff > 0 sum only nchunks_h slabs */
+    int32_t nchunks_h, pad;
 } mgn_wgrad_reduce;
 size_t mgn_block_backward_keep_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node);
 int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,

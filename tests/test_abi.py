@@ -58,7 +58,9 @@ int main(void) {
   printf("mgn_pack_job %zu\n", sizeof(mgn_pack_job));
   P(mgn_topology, row_perm) P(mgn_mlp, wpack) P(mgn_mlp, bias) P(mgn_mlp, scale)
   P(mgn_mlp_saved, rden) P(mgn_block_saved, node) P(mgn_block_saved, aggr) P(mgn_pack_job, n)
-  P(mgn_mlp, norm_dim) P(mgn_pack_job, n_src) P(mgn_pack_job, kb_pad)
+  P(mgn_mlp, norm_dim) P(mgn_pack_job, n_src) P(mgn_pack_job, kb_pad) P(mgn_block_saved, proj)
+  printf("mgn_wgrad_reduce %zu\n", sizeof(mgn_wgrad_reduce));
+  P(mgn_wgrad_reduce, nchunks_x) P(mgn_wgrad_reduce, hoff) P(mgn_wgrad_reduce, nchunks_h)
   return 0;
 }
 """
@@ -85,12 +87,16 @@ int main(void) {
     assert int(got["mgn_mlp.norm_dim"]) == nat.Mlp.norm_dim.offset
     assert int(got["mgn_pack_job.n_src"]) == nat.PackJob.n_src.offset
     assert int(got["mgn_pack_job.kb_pad"]) == nat.PackJob.kb_pad.offset
+    assert int(got["mgn_block_saved.proj"]) == nat.BlockSaved.proj.offset
+    assert int(got["mgn_wgrad_reduce"]) == ctypes.sizeof(nat.WgradReduce)
+    for f in ("nchunks_x", "hoff", "nchunks_h"):
+        assert int(got["mgn_wgrad_reduce." + f]) == getattr(nat.WgradReduce, f).offset
 
 
 def test_host_size_functions(lib):
     from graphphysics import _native as nat
 
-    assert lib.mgn_abi_version() == 15
+    assert lib.mgn_abi_version() == 16
     # fragment-packed Linear: max(fwd, transposed) fragment count x 64 lanes x VEC
     assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_BF16) == max(8 * 12, 24 * 4) * 64 * 8
     assert lib.mgn_linear_pack_elems(2, 128, nat.MGN_F32) == max(1 * 32, 8 * 1) * 64

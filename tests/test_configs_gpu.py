@@ -320,6 +320,10 @@ def _libmgn_eval(x, ei, ea, gy, mp, h, dtype, node_in, edge_in, out, masks=None)
     return res
 
 
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-300))
+
+
 def _pinned_eval(ref, x, ei, ea, gy, mp, masks, stats):
     """_aten_eval in fp64 on libmgn's ReLU branch (tests/_masks.py; checkpointed blocks)."""
     from torch.utils.checkpoint import checkpoint

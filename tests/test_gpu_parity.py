@@ -1194,3 +1194,45 @@ def test_concurrent_weight_gradients_match_one_stream(dtype, caps, batch):
             assert torch.equal(a, c)
         else:
             assert relerr(c, a) <= 1e-6, relerr(c, a)
+
+
+@pytest.mark.parametrize("batch,conc", [(2, "0"), (8, "auto"), (1, "0,0")])
+def test_recomputed_edge_weight_gradients_match_saved_inputs(batch, conc):
+    """mgn_block_saved.proj (ABI v16, _engine.REW): the training forward writes no R8 inputs of the edge
+    MLP's hidden layers and the backward's chain16_rew_kernel recomputes X1..X3 from e and the block's
+    node projections with the forward's own operations. Outputs and input gradients are bit-identical
+    to the saved-input path (the data gradients never read the saves). Parameter gradients: the same
+    products summed in another order (the recomputed launch's 32-row steps and its own slab partition,
+    the ring re-balanced without the three edge jobs) — fp32 rounding only, rel-L2 <= 1e-5 (measured
+    <= 2.5e-7). Against fp64 at full size: test_configs_gpu's aneurysm gradients (MGN_REW=auto recomputes
+    there: 1.4M edges)."""
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils import meshes
+    from graphphysics.utils.data import Data
+
+    b = meshes.cylinder_batch(batch, jitter=0.01)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(b["x"].shape[0], 11, generator=gen).to(DEV).requires_grad_(True)
+    ea = torch.from_numpy(b["edge_attr"]).to(DEV).requires_grad_(True)
+    g = Data(x=x, edge_index=torch.from_numpy(b["edge_index"]).to(DEV), edge_attr=ea)
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(4, 11, 3, 2, 128, compute_dtype=torch.bfloat16).to(DEV)
+    runs = []
+    for rew in ("0", "1"):
+        _engine.REW, _engine.CONC_WGRAD = rew, conc
+        try:
+            y = m(g)
+            y.backward(torch.ones_like(y))
+            torch.cuda.synchronize()
+            runs.append((y.detach().clone(), x.grad.clone(), ea.grad.clone(), [p.grad.clone() for p in m.parameters()]))
+            m.zero_grad(set_to_none=True)
+            x.grad = ea.grad = None
+        finally:
+            _engine.REW, _engine.CONC_WGRAD = "auto", "auto"
+    (y0, gx0, ge0, p0), (y1, gx1, ge1, p1) = runs
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1) and torch.equal(ge0, ge1)
+    worst = max(relerr(c, a) for a, c in zip(p0, p1))
+    print(f"recomputed vs saved inputs: worst parameter-gradient rel-L2 {worst:.2e}")
+    assert worst <= 1e-5, worst

@@ -12,7 +12,7 @@ EXTRA=""
 IN=${SRCFILE:-graph-physics_amd/csrc/$SRC}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable $EXTRA $2 -I include -I graph-physics_amd/csrc -c $IN -o $L/var/${B}_$1.o
 OBJS=""
-for s in mgn_mlp mgn_chain16 mgn_graph mgn_build mgn_prof; do
+for s in mgn_mlp mgn_chain16 mgn_rew mgn_graph mgn_build mgn_prof; do
   if [ $s = $B ]; then OBJS="$OBJS $L/var/${B}_$1.o"; else OBJS="$OBJS $L/$s.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS -o $L/var/libmgn_$1.so

@@ -19,7 +19,8 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HOT_SOURCES = ["mgn_common.h", "mgn_chain.h", "mgn_mlp.hip", "mgn_chain16.hip", "mgn_graph.hip"]
+HOT_SOURCES = ["mgn_common.h", "mgn_chain.h", "mgn_chain16_dev.h", "mgn_mlp.hip", "mgn_chain16.hip", "mgn_rew.hip",
+               "mgn_graph.hip"]
 SIMDS = 256 * 4  # MI355X: 256 CUs x 4 SIMDs
 XCDS = 8
 
@@ -44,7 +45,7 @@ def kernel_class(name):
                      ("chain16_fwd_kernel", "fwd_edge"), ("chain16_bwd_kernel", "bwd_edge"),
                      ("edge_fwd_f32_chain_kernel", "fwd_edge"), ("edge_bwd_f32_chain_kernel", "bwd_edge"),
                      ("mlp_wgrad_kernel", "wgrad_dense"), ("wgrad_ring_kernel", "wgrad"),
-                     ("wgrad_ring_f32_kernel", "wgrad"),
+                     ("wgrad_ring_f32_kernel", "wgrad"), ("chain16_rew_kernel", "wgrad"),
                      ("wgrad_reduce_kernel", "wgrad_reduce"), ("node_grad_kernel", "combine"),
                      ("node_proj_kernel", "proj"), ("adamw", "adamw"), ("pack_kernel", "pack")):
         if key in name:

@@ -6,7 +6,7 @@ from collections import defaultdict
 rows = defaultdict(list)
 for line in open(sys.argv[1], errors="replace"):
     p = line.split()
-    if len(p) == 13 and p[0] in ("fwd16", "bwd16", "nfwd16", "nbwd16", "f32f", "f32b", "gfe", "gfn", "gfd", "gbe", "gbn", "gwg"):
+    if len(p) == 13 and p[0] in ("fwd16", "bwd16", "nfwd16", "nbwd16", "f32f", "f32b", "gfe", "gfn", "gfd", "gbe", "gbn", "gwg", "f32nf", "f32nb"):
         rows[p[0]].append([int(v) for v in p[1:]])
 stage = sorted(int(l.split()[1]) for l in open(sys.argv[1], errors="replace") if l.startswith("nfwd16_stage "))
 if stage:
