@@ -69,18 +69,37 @@ def load(path):
     return per
 
 
-def replay_classes(trace_csv, steps):
+def block_wgrad(name, launches_per_step, mp):
+    """The generic kernels' weight-gradient launch of a processor block (block_wgrad_generic: one multi-job
+    mlp_wgrad_kernel launch per block, hidden 16/32/64 — Cfg A, Cfg C) is bench.py's class "wgrad", like
+    the ring of the h=128 blocks; the encoders' / decoder's mlp_wgrad_kernel launches stay "wgrad_dense".
+    Told apart by their count: MP launches per step."""
+    return "mlp_wgrad_kernel" in name and mp and abs(launches_per_step - mp) < 1e-9
+
+
+def _mp(workload):
+    m = re.search(r":mp(\d+):", ":" + (workload or "") + ":")
+    return int(m.group(1)) if m else None
+
+
+def replay_classes(trace_csv, steps, workload=None):
     """Per-class device time of the last `steps` REPLAYED steps of a rocprofv3 kernel trace (a step
     starts at its preamble_stats launch, as tools/gap_summary.py): {class: {us_per_step, launches_per_step,
     avg_us}} — what bench.py picks its dominant kernel class from (the replay, not eager steps)."""
     rows = sorted(csv.DictReader(open(trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("preamble_stats")]
     seg = rows[starts[-steps]:]
+    mp = _mp(workload)
+    count = {}
+    for r in seg:
+        count[instance_key(r)] = count.get(instance_key(r), 0) + 1
     agg = {}
     for r in seg:
         c = kernel_class(r["Kernel_Name"])
         if c is None:
             continue
+        if block_wgrad(r["Kernel_Name"], count[instance_key(r)] / steps, mp):
+            c = "wgrad"
         agg.setdefault(c, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     return {c: {"us_per_step": round(sum(v) / steps, 2), "launches_per_step": len(v) / steps,
                 "avg_us": round(sum(v) / len(v), 2)} for c, v in agg.items()}
@@ -127,11 +146,17 @@ def main(workload, out, fetch_csv, write_csv, sq_csv=None, trace_csv=None, steps
             if d.get("GRBM_GUI_ACTIVE"):
                 d["implied_clock_mhz"] = round(d["GRBM_GUI_ACTIVE"] / XCDS / durs[key], 0)
         res[key] = d
+    # processor blocks' generic weight-gradient launches: class "wgrad" (block_wgrad); steps profiled =
+    # AdamW launches (one per step)
+    nsteps = sum(d.get("launches", 0) for d in res.values() if d["class"] == "adamw")
+    for d in res.values():
+        if nsteps and block_wgrad(d["kernel"], d.get("launches", 0) / nsteps, _mp(workload)):
+            d["class"] = "wgrad"
     doc = {"sources_sha": sources_sha(), "workload": workload, "fetch_correction": 2.0,
            "unit": "per launch (median over launches)", "kernels": res,
            "schedule": schedule or "default (MGN_CONC_WGRAD=auto)"}
     if trace_csv:
-        doc["replay"] = replay_classes(trace_csv, int(steps))
+        doc["replay"] = replay_classes(trace_csv, int(steps), workload)
         doc["replay_source"] = "rocprofv3 --kernel-trace of the same bench command, last %s replayed steps" % steps
     json.dump(doc, open(out, "w"), indent=1)
     for k, d in res.items():
