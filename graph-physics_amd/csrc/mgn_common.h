@@ -124,8 +124,8 @@ __host__ __device__ __forceinline__ int rup(int a, int b) { return cdiv(a, b) * 
 //   image[((nt*8 + t)*64 + lane)*4 + r]  = W[nt*16 + (lane&15)][t*16 + 4*(lane>>4) + r]   (forward)
 //   imageT[((kt*8 + t)*64 + lane)*4 + r] = W[t*16 + 4*(lane>>4) + r][kt*16 + (lane&15)]   (transposed)
 // — one such image per 128-column block of the input (round 5: the chained fp32 node MLP's layer 0
-// reads both blocks of its [x ‖ aggr] weight), block b's image of columns 128b .. 128b + 127 at
-// chain_image_off(n, k, b) (mgn_mlp.hip).
+// reads both blocks of its [x ‖ aggr] weight, the next block's projections the x_i / x_j blocks of the
+// edge W0), block b's image of columns 128b .. 128b + 127 at chain_image_off(n, k, b) (mgn_mlp.hip).
 __host__ __device__ inline int chain_images(int n, int k, int dtype) {
     return dtype == MGN_F32 && n == 128 && k > 0 && k % 128 == 0 ? k / 128 : 0;
 }

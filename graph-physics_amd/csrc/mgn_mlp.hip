@@ -347,6 +347,10 @@ struct FwdArgs {
     int32_t r0_elems;  // LDS region 0 (layer-0 input / odd-layer activations / fp32 z staging), in T
     int32_t wl_elems;  // WL kernels: LDS element offset of the staged weights
     WlDesc wl;
+    // chained fp32 node MLP: the NEXT block's node projections P = [x_out·W0bᵀ ‖ x_out·W0cᵀ] (fp32
+    // [N][2H], what node_proj_kernel writes) from the next edge MLP's forward pack (nullptr: none)
+    const float* pn_pack;
+    float* pn_out;
 };
 
 // Diagnostic ablation mask for timing studies (results are wrong when nonzero): a compile-time
@@ -2255,6 +2259,9 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
 #ifndef MGN_F32N_AG
 #define MGN_F32N_AG 4  // in-edges gathered per round trip by the fp32 aggregation
 #endif
+#ifndef MGN_F32N_PROJ
+#define MGN_F32N_PROJ 1  // the chained fp32 node MLP computes the next block's projections (A/B builds: 0)
+#endif
 constexpr int F32N_WAVES = 4;  // one wave per SIMD, 64 rows per workgroup
 #define F32N_BOUNDS __launch_bounds__(F32N_WAVES * 64, 1)
 constexpr size_t F32N_LDS_FWD = (2 * F32C_LAYER + 5 * 128) * sizeof(float);
@@ -2380,6 +2387,8 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) acc[nt] = *reinterpret_cast<const f4*>(vec + l * H + 16 * nt + 4 * g);
         float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
+        if (l == 3 && a.pn_pack)  // the next block's W0b image streams in under the last layer
+            f32n_stage(a.pn_pack + chain_image_off(H, 3 * H, 1), img1);
         f32c_gemm(acc, x1, cur, lane, sv + r8);  // its input's R8 save, under the MFMAs
         F32C_STAMP(1);
         if (l < 3) {
@@ -2414,6 +2423,27 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
                 st4(reinterpret_cast<float*>(a.z_save) + row * H + n, acc[nt]);
                 st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
             }
+            x1[nt] = valid ? y : f4{0.f, 0.f, 0.f, 0.f};  // x_out: the projections' B operand
+        }
+    }
+    if (!a.pn_pack) return;
+    // the NEXT block's node projections from x_out (reference layers.py:689-690,717 applied per node:
+    // [e ‖ x_i ‖ x_j]·W0ᵀ = e·W0aᵀ + (x·W0bᵀ)[dst] + (x·W0cᵀ)[src]), W0b from img1, W0c from img0
+    f32c_stage_wait();
+    __syncthreads();  // W0b landed; every wave is done with img0 (layer 3)
+    f32n_stage(a.pn_pack + chain_image_off(H, 3 * H, 2), img0);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+        f32c_gemm(acc, x1, half ? img0 : img1, lane);
+        if (valid) {
+#pragma unroll
+            for (int nt = 0; nt < 8; ++nt) st4(a.pn_out + row * (2 * H) + half * H + 16 * nt + 4 * g, acc[nt]);
+        }
+        if (half == 0) {
+            f32c_stage_wait();
+            __syncthreads();
         }
     }
     F32C_STAMP(4);
@@ -2609,6 +2639,9 @@ struct MlpIn {
     const float* proj;    // EDGE: node projections (see FwdArgs)
     const int32_t* proj_i;
     const int32_t* proj_j;
+    const float* pn_pack; // NODE, fp32 h=128: the next block's projections (FwdArgs), if the chained kernel runs
+    float* pn_out;
+    int* pn_done;         // set to 1 when they were computed
 };
 
 template <class T, int H, int MODE>
@@ -2684,6 +2717,11 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
             const int grid = (int)(rows_pad(M) / (16 * F32N_WAVES));
             if (grid == 0) return 0;
             if (int e = set_lds((const void*)node_fwd_f32_chain_kernel, F32N_LDS_FWD)) return e;
+            if (in.pn_pack && in.pn_out) {
+                a.pn_pack = in.pn_pack;
+                a.pn_out = in.pn_out;
+                if (in.pn_done) *in.pn_done = 1;
+            }
             ProfScope ps(PROF_FWD_NODE, st);
             hipLaunchKernelGGL(node_fwd_f32_chain_kernel, dim3(grid), dim3(F32N_WAVES * 64), F32N_LDS_FWD, st, a);
             MGN_LAUNCH_CHECK();
@@ -4056,7 +4094,8 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     float* proj = reinterpret_cast<float*>(ws);
     const bool chain = chain_eligible(edge);
     const float* b0 = chain ? edge->bias[0] : nullptr;  // the chained kernel takes b0 from P_i
-    MGN_REQUIRE(!proj_ready || chain, "proj_ready: the workspace holds bf16 projections of the chained path only");
+    MGN_REQUIRE(!proj_ready || chain || dt == MGN_F32,
+                "proj_ready: the workspace holds the projections of the chained bf16 path or of the fp32 node MLP");
     // Small graphs on the generic kernels (hidden <= 64): layer 0 as the reference's single K = 3h
     // product over the gathered [e ‖ x_i ‖ x_j] rows (layers.py:689-690) — the node-projection launch
     // would cost more than the 4h² FLOPs per edge it saves (cylinder.json / plate.json sizes)
@@ -4108,9 +4147,23 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
     memset(&nin, 0, sizeof(nin));
     nin.seg[0] = SrcSeg{x, nullptr, H, H, dt, 0, 0};
     nin.nseg = 1;
+    // fp32 h=128: the chained node kernel also computes the next block's node projections (the next
+    // call skips its projection launch)
+    int pn_done = 0;
+    if (MGN_F32N_PROJ && dt == MGN_F32 && H == 128 && next_edge && next_ws && next_edge->dtype == MGN_F32 &&
+        next_edge->hidden == H &&
+        next_edge->in_dim == 3 * H && next_ws_bytes >= block_fwd_ws(t, next_edge) && t->num_nodes > 0 &&
+        t->num_edges > 0) {
+        nin.pn_pack = reinterpret_cast<const float*>(next_edge->wpack);
+        nin.pn_out = reinterpret_cast<float*>(next_ws);
+        nin.pn_done = &pn_done;
+    }
     // K0 = 2H: the aggregation fills columns [H, 2H) inside the kernel
-    return mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
-                       saved->aggr, st);
+    if (int r = mlp_fwd_any(node, MODE_NODE, nin, t->num_nodes, x_out, dt, H, x, &saved->node, t, edge, &saved->edge,
+                            saved->aggr, st))
+        return r;
+    if (pn_done && next_proj_ready) *next_proj_ready = 1;
+    return 0;
 }
 
 int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x, const void* e,
