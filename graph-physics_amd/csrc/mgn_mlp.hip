@@ -3220,9 +3220,8 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     constexpr int H = 128;
     constexpr bool F32 = sizeof(T) == 4;
     const int64_t RPE = rows_pad(in.E), RPN = rows_pad(in.N);
-    auto rows_for = [](int64_t RP, int64_t target, int* nch) {
+    auto rows_for = [](int64_t RP, int64_t target, int* nch, int64_t cmax) {
         int64_t c = cdiv64(RP, target);
-        const int64_t cmax = wgrad_max_chunks(RP);
         if (c > cmax) c = cmax;
         if (c < 1) c = 1;
         int64_t r = cdiv64(cdiv64(RP, c), 64) * 64;
@@ -3233,7 +3232,7 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     // chunks, 5 node jobs on cn chunks, the 2 W0-projection jobs (node rows, into the edge slabs'
     // x-block columns) on cp ≈ cn chunks — the reduction sums only the first cp slabs of those
     // columns (RedDesc x-columns), so the projections need not be cut into ce short chunks. The
-    // edge slab buffer holds wgrad_max_chunks(RPE) slabs (keep_layout, mlp_bwd_ws): cp is capped
+    // edge slab buffer holds slab_chunks(RPE) slabs (keep_layout, mlp_bwd_ws): cp is capped
     // there (graphs with more nodes than edges).
     const int cus = wgrad_cus();
     // recomputed edge layers 1..3 (chain16_edge_wgrad_recompute): their own launch ahead of the ring,
@@ -3252,14 +3251,18 @@ int block_wgrad_ring(const mgn_mlp* edge, const mgn_mlp* node, const BlockWgradI
     }
     int ce = 1, cn = 1, cp = 1;
     int re = 0, rn = 0, rp = 0;
+    // chunks per job up to the slab buffers' capacity (keep_layout / mlp_bwd_ws: slab_chunks) — with the
+    // recomputed layers the edge MLP keeps ONE ring job, which needs more than 64 chunks to fill the
+    // chip on large graphs (Cfg E: 64 chunks of 21.8k rows ran 326 µs on 64 CUs)
+    const int64_t cemax = slab_chunks(RPE, edge), cnmax = slab_chunks(RPN, node);
     {
         const int64_t total = ejobs * RPE + 7 * RPN;
         for (int64_t target = cdiv64(cdiv64(total, cus), 64) * 64;; target += 64) {
-            re = rows_for(RPE, target, &ce);
-            rn = rows_for(RPN, target, &cn);
+            re = rows_for(RPE, target, &ce, cemax);
+            rn = rows_for(RPN, target, &cn, cnmax);
             if (ejobs * ce + 7 * cn <= cus || (ce == 1 && cn == 1)) break;
         }
-        const int64_t cpmax = wgrad_max_chunks(RPE);
+        const int64_t cpmax = cemax;
         const int64_t c = cn < cpmax ? cn : cpmax;
         rp = (int)(cdiv64(cdiv64(RPN, c), 64) * 64);
         cp = (int)cdiv64(RPN, rp);
@@ -4269,7 +4272,7 @@ static KeepLayout keep_layout(const mgn_topology* t, const mgn_mlp* edge, const 
     k.ndsp = o;
     o += align_up((size_t)(RPN / 16) * node->out_dim * sizeof(float));
     k.npart = o;
-    o += align_up((size_t)wgrad_max_chunks(RPN, node->hidden) * grad_G(node) * sizeof(float));
+    o += align_up((size_t)slab_chunks(RPN, node) * grad_G(node) * sizeof(float));
     k.total = o;
     return k;
 }
