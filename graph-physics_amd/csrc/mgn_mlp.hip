@@ -2582,18 +2582,30 @@ __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
 }
 
 // --------------------------------------------------------------------------- host side
+// Round 5 (small graphs): the generic bf16 kernels on 32-row edge / dense and 16-row
+// node workgroups — twice / four times the workgroups of a small graph's launch, each a shorter chain
+// (Cfg C at plate.json's sizes 1,032 -> 1,166 steps/s same box, `profiles/r05_ab.txt`; Cfg B's bf16
+// generic launch, the decoder, measured neutral at 32 rows in round 2). fp32 keeps 32 / 32: the fp32
+// node MLP's chained backward writes its RMSNorm-scale partials per 32 rows, and 16 rows bought Cfg A
+// (fp32 h=32) only +0.9 %.
 #ifndef MGN_BF16_BM
-#define MGN_BF16_BM 64  // rows per workgroup of the generic bf16 dense / edge kernels (A/B builds: 32)
+#define MGN_BF16_BM 32  // rows per workgroup of the generic bf16 dense / edge kernels (A/B builds: 64)
 #endif
 #ifndef MGN_F32_BM
 #define MGN_F32_BM 32  // rows per workgroup of the generic fp32 dense / edge kernels (A/B builds: 64)
 #endif
+#ifndef MGN_NODE_BM16
+#define MGN_NODE_BM16 16  // rows per workgroup of the generic bf16 node-MLP kernels (A/B builds: 32)
+#endif
 template <class T>
 constexpr int bm_of() { return sizeof(T) == 4 ? MGN_F32_BM : MGN_BF16_BM; }
-// rows per workgroup tile: node MLPs use 32 (N is ~6x smaller than E: twice the workgroups)
+// rows per workgroup tile: node MLPs use 32 rows in fp32 and MGN_NODE_BM16 in bf16 (N is ~6x smaller than
+// E: more, shorter workgroups)
 template <class T, int MODE>
-constexpr int bm_for() { return MODE == MODE_NODE ? 32 : bm_of<T>(); }
-int bm_host(int dtype, int mode) { return mode == MODE_NODE ? 32 : dtype == MGN_F32 ? MGN_F32_BM : MGN_BF16_BM; }
+constexpr int bm_for() { return MODE == MODE_NODE ? (sizeof(T) == 4 ? 32 : MGN_NODE_BM16) : bm_of<T>(); }
+int bm_host(int dtype, int mode) {
+    return mode == MODE_NODE ? (dtype == MGN_F32 ? 32 : MGN_NODE_BM16) : dtype == MGN_F32 ? MGN_F32_BM : MGN_BF16_BM;
+}
 
 // Raise a kernel's dynamic-LDS limit once (not per launch: launches may be inside a graph capture).
 int set_lds(const void* fn, size_t bytes) {
