@@ -1236,3 +1236,43 @@ def test_recomputed_edge_weight_gradients_match_saved_inputs(batch, conc):
     worst = max(relerr(c, a) for a, c in zip(p0, p1))
     print(f"recomputed vs saved inputs: worst parameter-gradient rel-L2 {worst:.2e}")
     assert worst <= 1e-5, worst
+
+
+@pytest.mark.parametrize("n,e", [(37, 190), (300, 1000), (3000, 700)])
+def test_recomputed_weight_gradients_on_small_graphs_vs_fp64(n, e):
+    """MGN_REW="1" far below the auto threshold: E not a multiple of the recompute's 32-row steps, one
+    row chunk, padded rows recomputed from a clamped row (their dZ is 0), more nodes than edges. Bound as
+    test_epd_bf16_h128_more_nodes_than_edges: 2 x PyTorch's bf16 autocast of the reference, vs fp64."""
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    g = torch.Generator().manual_seed(13)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(e, 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    mp, h = 3, 128
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, h)
+    rp = dict(ref.named_parameters())
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    y64 = O.encode_process_decode(x.double(), ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = O.encode_process_decode(x, ei, ea, pac, mp)
+    (yac.float() * gy).sum().backward()
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, h, compute_dtype=torch.bfloat16).to(DEV)
+    _engine.REW = "1"
+    try:
+        y = m(Data(x=x.to(DEV), edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+        (y * gy.to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        _engine.REW = "auto"
+    assert relerr(y, y64) <= 2 * relerr(yac, y64)
+    for k, p in m.named_parameters():
+        assert torch.isfinite(p.grad).all(), k
+        assert relerr(p.grad, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
