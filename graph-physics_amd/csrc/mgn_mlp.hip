@@ -934,6 +934,11 @@ constexpr int WG_GROUPS = 2;
 #ifndef MGN_WG_PER_CU32
 #define MGN_WG_PER_CU32 2
 #endif
+// fp32 weight-gradient operands loaded as 16-byte row quads (A/B builds: 0 = one 4-byte fragment
+// per k-step)
+#ifndef MGN_WG_QUAD
+#define MGN_WG_QUAD 1
+#endif
 
 template <class T, int H>
 size_t wgrad_lds_bytes(bool staged) {
@@ -953,7 +958,9 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     constexpr int LDT = SR + CH;                // LDS row = one input column over SR rows (+pad)
     using C = TileCfg<NT, NT>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int grp = threadIdx.x / MGN_THREADS, tid = threadIdx.x % MGN_THREADS;
+    // group and wave index wave-uniform (readfirstlane): the row loops below then run on scalar
+    // counters, without exec-masked exits
+    const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / MGN_THREADS), tid = threadIdx.x % MGN_THREADS;
     T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * H * LDT;  // this group's [2][H][LDT]
     F32C_STAMP_DECL;
     const WgJob job = a.job[blockIdx.y];
@@ -972,7 +979,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     };
     const int64_t r_begin = (int64_t)blockIdx.x * RPC;
     const int64_t r_end = r_begin + RPC < RP ? r_begin + RPC : RP;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int nt0 = wn * C::NTW, mt0 = wm * C::MTW;
     const bool active = mt0 < NT;
@@ -1011,7 +1018,58 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     // group runs the same iteration count (a group past the end stages zeros) so all threads reach
     // each barrier. Loads past r_end are clamped to a valid stage and never consumed.
     constexpr int KS = SR / KSTEP;
-    auto pipeline = [&](auto&& issue_x, auto&& commit_x, auto&& frag_b) {
+    auto pipeline = [&](auto&& issue_x, auto&& commit_x, auto&& frag_b, auto&& frag_b4) {
+      if constexpr (VEC == 1 && MGN_WG_QUAD && H <= 64) {
+        // fp32: dZ as 16-byte row quads (see the direct path below) and the staged X read back as
+        // the same quads (4 consecutive rows of a column in the [col][row] image: one ds_read_b128)
+        constexpr int KQ = SR / 16;
+        const int g4 = lane >> 4;
+        f4 zq[KQ][C::NTW];
+        auto issue_z = [&](int64_t m0) {
+            const int64_t mc = m0 < r_end ? m0 : r_begin;
+#pragma unroll
+            for (int q = 0; q < KQ; ++q)
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+                    zq[q][i] = *reinterpret_cast<const f4*>(
+                        reinterpret_cast<const float*>(Z) + (((mc + q * 16) >> 3) + (g4 >> 1)) * H * 8 +
+                        (int64_t)((nt0 + i) * 16 + (lane & 15)) * 8 + 4 * (g4 & 1));
+        };
+        issue_x(r_begin + grp * SR);
+        issue_z(r_begin + grp * SR);
+        for (int64_t base = r_begin; base < r_end; base += WG_GROUPS * SR) {
+            const int64_t m0 = base + grp * SR;
+            const int par = (int)((base - r_begin) / (WG_GROUPS * SR) & 1);
+            commit_x(par);
+            f4 za[KQ][C::NTW];
+#pragma unroll
+            for (int q = 0; q < KQ; ++q)
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i) za[q][i] = zq[q][i];
+            __syncthreads();
+            issue_x(m0 + WG_GROUPS * SR);
+            issue_z(m0 + WG_GROUPS * SR);
+            if (active && m0 < r_end) {
+#pragma unroll
+                for (int q = 0; q < KQ; ++q) {
+                    f4 xb[C::MTW];
+#pragma unroll
+                    for (int j = 0; j < C::MTW; ++j) xb[j] = kon[j] ? frag_b4(par, q, j) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        typename Mf<T>::frag fa[C::NTW];
+#pragma unroll
+                        for (int i = 0; i < C::NTW; ++i) fa[i] = za[q][i][v];
+#pragma unroll
+                        for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                            for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], xb[j][v], acc[i][j]);
+                        if (do_bias) bias_acc(fa);
+                    }
+                }
+            }
+        }
+      } else {
         typename Mf<T>::frag zn[KS][C::NTW];
         auto issue_z = [&](int64_t m0) {
             const int64_t mc = m0 < r_end ? m0 : r_begin;
@@ -1049,7 +1107,9 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 }
             }
         }
+      }
     };
+    auto no_b4 = [](int, int, int) { return f4{0.f, 0.f, 0.f, 0.f}; };  // bf16-only pipelines
     if (!staged && VEC == 8) {
         // R8 input: the 4 waves of a group all need the same 8 X fragments per k-step, so the
         // group copies each stage once (SR/8 octets x H columns x 16 B, coalesced: in R8 an
@@ -1081,7 +1141,65 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 const u32x4* buf = img + (size_t)par * ITEMS;
                 return ld_frag(reinterpret_cast<const T*>(buf + (ks * (KSTEP / 8) + (lane >> 4)) * H + (mt0 + j) * 16 +
                                                           (lane & 15)));
-            });
+            },
+            no_b4);
+    } else if (!staged && VEC == 1 && MGN_WG_QUAD) {
+        if constexpr (VEC == 1) {
+            // fp32 R8 operands as 16-byte quads: lane (g, f) = (lane >> 4, lane & 15) loads rows
+            // 4g..4g+3 of a 16-row step of feature f (one f4: R8 keeps a feature's 8 rows contiguous),
+            // so a wave's load is 1 KiB of whole 128-byte lines; k-step v of the quad then pairs
+            // row 4g+v of dZ and X in lane (g, f). A 4-byte fragment load per k-step (lanes 32 B
+            // apart) cost the texture addresser one cache access per lane: 64 per load, and the
+            // launch was address-bound (Cfg A: 10.2M L1 accesses for 159k loads). Same products,
+            // summed over the rows in another order. A ring of PQ quads per operand stays in flight.
+            constexpr int PQ = H <= 32 ? 4 : H <= 64 ? 2 : 1;
+            constexpr int64_t QSTEP = (int64_t)WG_GROUPS * 16;
+            const int g4 = lane >> 4, fl = lane & 15;
+            const int cz = fl < job.kp ? fl : 0;
+            auto qidx = [&](int64_t m, int c, int64_t cols) {
+                return ((m >> 3) + (g4 >> 1)) * cols * 8 + (int64_t)c * 8 + 4 * (g4 & 1);
+            };
+            f4 qa[PQ][C::NTW], qb[PQ][C::MTW];
+            auto load = [&](int64_t m0, f4 (&fa)[C::NTW], f4 (&fb)[C::MTW]) {
+                const int64_t m = m0 < r_end ? m0 : r_begin;
+#pragma unroll
+                for (int i = 0; i < C::NTW; ++i)
+                    fa[i] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(Z) + qidx(m, (nt0 + i) * 16 + fl, H));
+#pragma unroll
+                for (int j = 0; j < C::MTW; ++j)
+                    fb[j] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(X) +
+                                                         qidx(m, kon[j] ? col0 + (mt0 + j) * 16 + fl : cz, job.kp));
+            };
+            const int64_t m_first = r_begin + grp * 16;
+            if (active && m_first < r_end) {
+                const int nq = (int)((r_end - m_first + QSTEP - 1) / QSTEP);
+#pragma unroll
+                for (int u = 0; u < PQ; ++u) load(m_first + u * QSTEP, qa[u], qb[u]);
+                for (int q0 = 0; q0 < nq; q0 += PQ) {
+#pragma unroll
+                    for (int u = 0; u < PQ; ++u) {
+                        const bool ok = q0 + u < nq;
+                        f4 za[C::NTW], xb[C::MTW];
+#pragma unroll
+                        for (int i = 0; i < C::NTW; ++i) za[i] = ok ? qa[u][i] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int j = 0; j < C::MTW; ++j) xb[j] = ok && kon[j] ? qb[u][j] : f4{0.f, 0.f, 0.f, 0.f};
+                        load(m_first + (int64_t)(q0 + u + PQ) * QSTEP, qa[u], qb[u]);
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            typename Mf<T>::frag fa[C::NTW];
+#pragma unroll
+                            for (int i = 0; i < C::NTW; ++i) fa[i] = za[i][v];
+#pragma unroll
+                            for (int i = 0; i < C::NTW; ++i)
+#pragma unroll
+                                for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], xb[j][v], acc[i][j]);
+                            if (do_bias) bias_acc(fa);
+                        }
+                    }
+                }
+            }
+        }
     } else if (!staged && MGN_WG_PF > 0) {
         // R8 operands straight from global memory (fp32: one VGPR per fragment): a register ring
         // keeps MGN_WG_PF k-steps of both operands in flight (the loop is unrolled by it so every
@@ -1094,24 +1212,33 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             const int64_t mr = (m0 < r_end ? m0 : r_begin) + VEC * (lane >> 4);
 #pragma unroll
             for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+            // unconditional loads (an inactive column block reads a valid column and is zeroed where
+            // consumed): a load-or-zero join would again make the compiler copy the ring registers
+            const int cz = (lane & 15) < job.kp ? (lane & 15) : 0;
 #pragma unroll
             for (int j = 0; j < C::MTW; ++j)
-                fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
+                fb[j] = ld_frag(X + r8_index(mr, kon[j] ? col0 + (mt0 + j) * 16 + (lane & 15) : cz, job.kp));
         };
         const int64_t m_first = r_begin + grp * KSTEP;
         if (active && m_first < r_end) {
+            // every slot of the ring is loaded and consumed unconditionally (a conditional exit
+            // inside the unrolled ring made the compiler copy the ring registers, waiting on each
+            // load right after issuing it: Cfg A's launch spent ~2k cycles per k-step); the steps
+            // past the chunk's end (the count padded to a multiple of PF) multiply zeros (+0 to
+            // every sum: same values)
+            const int nsteps = (int)((r_end - m_first + STEP - 1) / STEP);
 #pragma unroll
             for (int u = 0; u < PF; ++u) load(m_first + u * STEP, ra[u], rb[u]);
-            for (int64_t m0 = m_first; m0 < r_end; m0 += PF * STEP) {
+            for (int s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
                 for (int u = 0; u < PF; ++u) {
-                    if (m0 + u * STEP >= r_end) break;
+                    const bool ok = s0 + u < nsteps;
                     typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
 #pragma unroll
-                    for (int i = 0; i < C::NTW; ++i) fa[i] = ra[u][i];
+                    for (int i = 0; i < C::NTW; ++i) fa[i] = ok ? ra[u][i] : zero;
 #pragma unroll
-                    for (int j = 0; j < C::MTW; ++j) fb[j] = rb[u][j];
-                    load(m0 + (u + PF) * STEP, ra[u], rb[u]);
+                    for (int j = 0; j < C::MTW; ++j) fb[j] = ok && kon[j] ? rb[u][j] : zero;
+                    load(m_first + (int64_t)(s0 + u + PF) * STEP, ra[u], rb[u]);
 #pragma unroll
                     for (int i = 0; i < C::NTW; ++i)
 #pragma unroll
@@ -1187,7 +1314,8 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                     typedef short s8 __attribute__((ext_vector_type(8)));
                     const s8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     return __builtin_bit_cast(typename Mf<T>::frag, v);
-                });
+                },
+                no_b4);
         }
     } else {
         // re-gathered layer-0 input: segment holding columns [col0, col0 + H) (segments are H
@@ -1227,6 +1355,11 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             [&](int par, int ks, int j) {
                 const T* buf = AT + (size_t)par * H * LDT;
                 return ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
+            },
+            [&](int par, int q, int j) {  // fp32 only: rows 16q + 4g .. +3 of the column
+                const T* buf = AT + (size_t)par * H * LDT;
+                return *reinterpret_cast<const f4*>(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + q * 16 +
+                                                    4 * (lane >> 4));
             });
     }
     F32C_STAMP(0);

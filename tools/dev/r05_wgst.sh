@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 5: generic weight-gradient launch stamps (libmgn_st: -DMGN_STAMPS on mgn_mlp.hip), Cfg A, 2 steps
+set -o pipefail
+L=graph-physics_amd/graphphysics/_lib
+cp $L/libmgn.so /tmp/libmgn_default.so
+cp $L/var/libmgn_st.so $L/libmgn.so
+timeout -k 10 300 python bench.py --mp 5 --hidden 32 --batch 1 --dtype fp32 --steps 2 --warmup 1 --cpu-steps 0 --no-mse --no-secondary --sustain 0 --no-profile > gpurun_out/wgst.log 2>&1
+rc=$?
+cp /tmp/libmgn_default.so $L/libmgn.so
+echo rc=$rc; grep -c "^gwgy" gpurun_out/wgst.log
