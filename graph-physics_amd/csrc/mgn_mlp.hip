@@ -472,6 +472,11 @@ __device__ __forceinline__ void fwd_last_epilogue(G& g, const FwdArgs& a, float*
     }
 }
 
+// in-edges per aggregation round trip of the generic node forward (A/B builds: 4 = groups of 4 and
+// the remainder one edge at a time, the round-4 form's round-trip count is higher)
+#ifndef MGN_GEN_AG
+#define MGN_GEN_AG 8
+#endif
 template <class T, int H, int BM, int MODE, bool WL = false>
 __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
     constexpr int KSTEP = Mf<T>::KSTEP;
@@ -503,26 +508,25 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_fwd_kernel(FwdArgs a) {
                 float s[CH];
 #pragma unroll
                 for (int v = 0; v < CH; ++v) s[v] = a.agg_scale ? a.agg_scale[c + v] : 1.f;
+                // groups of MGN_GEN_AG in-edges, every load of a group issued before its adds (one
+                // round trip per group; edges past the segment end re-read its last edge and are not
+                // added): the same sums in edge order as one edge at a time
+                constexpr int AG = MGN_GEN_AG;
                 const int kb = a.seg_ptr[row], ke = a.seg_ptr[row + 1];
-                int k = kb;
-                for (; k + 4 <= ke; k += 4) {
-                    float zz[4][CH], q[4];
+                for (int k = kb; k < ke; k += AG) {
+                    float zz[AG][CH], q[AG];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        Chunk<T>::load(z + (int64_t)(k + u) * H + c, zz[u]);
-                        q[u] = a.agg_rden[k + u];
+                    for (int u = 0; u < AG; ++u) {
+                        const int ku = k + u < ke ? k + u : ke - 1;
+                        Chunk<T>::load(z + (int64_t)ku * H + c, zz[u]);
+                        q[u] = a.agg_rden[ku];
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
+                    for (int u = 0; u < AG; ++u)
+                        if (k + u < ke) {
 #pragma unroll
-                        for (int v = 0; v < CH; ++v) acc[v] += s[v] * (zz[u][v] / q[u]);
-                }
-                for (; k < ke; ++k) {
-                    float zz[CH];
-                    Chunk<T>::load(z + (int64_t)k * H + c, zz);
-                    const float q = a.agg_rden[k];
-#pragma unroll
-                    for (int v = 0; v < CH; ++v) acc[v] += s[v] * (zz[v] / q);
+                            for (int v = 0; v < CH; ++v) acc[v] += s[v] * (zz[u][v] / q[u]);
+                        }
                 }
                 Chunk<T>::store(reinterpret_cast<T*>(a.agg_save) + row * H + c, acc);
             }
