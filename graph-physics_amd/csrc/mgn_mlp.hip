@@ -3781,6 +3781,9 @@ __global__ __launch_bounds__(MGN_THREADS) void node_proj_kernel(ProjArgs a) {
     }
 }
 
+#ifndef MGN_COMB_IDXPF
+#define MGN_COMB_IDXPF 1  // node_grad: source-direction edge ids prefetched one group ahead (A/B builds: 0)
+#endif
 #ifndef MGN_COMB_PAIR
 #define MGN_COMB_PAIR 0  // 1: node_grad's segment-sum items two at a time (A/B builds)
 #endif
@@ -3912,23 +3915,46 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
         float acc[CH];
 #pragma unroll
         for (int e = 0; e < CH; ++e) acc[e] = 0.f;
+        if (s == 0 || !MGN_COMB_IDXPF) {
 #pragma unroll 1
-        for (int k = kb; k < ke; k += SG) {
-            int64_t src[SG];
+            for (int k = kb; k < ke; k += SG) {
+                int64_t src[SG];
 #pragma unroll
-            for (int u = 0; u < SG; ++u) {
-                const int ku = k + u < ke ? k + u : ke - 1;
-                src[u] = s == 0 ? (int64_t)ku : (int64_t)a.row_perm[ku];
-            }
-            float t[SG][CH];
-#pragma unroll
-            for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
-#pragma unroll
-            for (int u = 0; u < SG; ++u)
-                if (k + u < ke) {
-#pragma unroll
-                    for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
+                for (int u = 0; u < SG; ++u) {
+                    const int ku = k + u < ke ? k + u : ke - 1;
+                    src[u] = s == 0 ? (int64_t)ku : (int64_t)a.row_perm[ku];
                 }
+                float t[SG][CH];
+#pragma unroll
+                for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + src[u] * H + c, t[u]);
+#pragma unroll
+                for (int u = 0; u < SG; ++u)
+                    if (k + u < ke) {
+#pragma unroll
+                        for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
+                    }
+            }
+        } else if (kb < ke) {
+            // source direction: the next group's edge ids (row_perm) load under this group's row
+            // loads, so a group costs one round trip instead of two (ids past the segment end clamp
+            // to its last edge; same sums in edge order)
+            int32_t id[SG];
+#pragma unroll
+            for (int u = 0; u < SG; ++u) id[u] = a.row_perm[kb + u < ke ? kb + u : ke - 1];
+#pragma unroll 1
+            for (int k = kb; k < ke; k += SG) {
+                float t[SG][CH];
+#pragma unroll
+                for (int u = 0; u < SG; ++u) Chunk<T>::load(dz + (int64_t)id[u] * H + c, t[u]);
+#pragma unroll
+                for (int u = 0; u < SG; ++u) id[u] = a.row_perm[k + SG + u < ke ? k + SG + u : ke - 1];
+#pragma unroll
+                for (int u = 0; u < SG; ++u)
+                    if (k + u < ke) {
+#pragma unroll
+                        for (int e = 0; e < CH; ++e) acc[e] += t[u][e];
+                    }
+            }
         }
         Chunk<T>::store(B + (size_t)r * a.ldb + s * a.HP + c, acc);
     }
