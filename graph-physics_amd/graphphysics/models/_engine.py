@@ -129,8 +129,8 @@ def conc_caps(E, chained, dev=None):
     CUs: 160 + 96; measured, Cfg B bf16: 332 -> 342 steps/s; 192 + 64: 297, 128 + 128: 322, both
     uncapped: 317). The CU count is the device's (a partitioned device or another SKU scales the split
     and the regime estimate). Measured slower, so one stream: fp32 Cfg B (its MFMA-bound ring: 98 ->
-    87), Cfg C at plate.json's sizes (1011 -> 942, uncapped), Cfg E (1.4M edges, throughput-bound: 33.5
-    -> 32.7). The small graphs lose to the cross-stream dependencies of the replayed graph even with one
+    87), Cfg C at plate.json's sizes (1011 -> 942, uncapped), Cfg E with saved edge inputs (1.4M edges,
+    throughput-bound: 33.5 -> 32.7; with the recomputed weight gradients it gains: see below). The small graphs lose to the cross-stream dependencies of the replayed graph even with one
     workspace per block (no wait on the main stream): Cfg A 1720 -> 1515 uncapped / 1420 at 160 + 96,
     Cfg C 1034 -> 870 / 883 (profiles/r04_ab.txt, r04_ab8.sh)."""
     v = CONC_WGRAD
@@ -141,6 +141,12 @@ def conc_caps(E, chained, dev=None):
         return d, r
     cus = _device_cus(dev)
     tiles_per_wave = E / (16 * 12 * cus)
+    if chained and tiles_per_wave > 4.0 and (REW == "1" or (REW == "auto" and E >= REW_MIN_EDGES)):
+        # throughput regime with the recomputed weight gradients (Cfg E): the chip split in halves
+        # (4 + 4 XCDs), measured 38.4 -> 39.4 steps/s; 160 + 96 and uncapped +1 %, splits off the
+        # 32-CU XCD grain (112 + 144, 144 + 112) -11 %, 192 + 64 -19 % (profiles/r05_ab.txt)
+        d = cus // 2
+        return d, cus - d
     if not (chained and 1.0 <= tiles_per_wave <= 4.0):
         return None
     d = (cus * 5 + 4) // 8
