@@ -279,3 +279,31 @@ def test_data_parallel_step_refuses_to_continue_after_validation_error():
                 ts._check_replicas()
         else:
             ts._check_replicas()
+
+
+def test_concurrent_backward_regimes(monkeypatch):
+    """conc_caps (models/_engine.py): which backward schedule each workload gets on a 256-CU device.
+    Cfg B (88,560 edges, 1.8 tiles per wave): 160 + 96; Cfg E (1,395,256 edges, recomputed weight
+    gradients): 128 + 128; the same graph with saved edge inputs (MGN_REW=0), small graphs and
+    generic (non-chained) blocks: one stream; explicit MGN_CONC_WGRAD settings pass through."""
+    from graphphysics.models import _engine as eng
+
+    monkeypatch.setattr(eng, "_device_cus", lambda dev=None: 256)
+    monkeypatch.setattr(eng, "CONC_WGRAD", "auto")
+    monkeypatch.setattr(eng, "REW", "auto")
+    assert eng.conc_caps(88560, True) == (160, 96)
+    assert eng.conc_caps(1395256, True) == (128, 128)
+    assert eng.conc_caps(11070, True) is None
+    assert eng.conc_caps(88560, False) is None
+    assert eng.conc_caps(1395256, False) is None
+    monkeypatch.setattr(eng, "REW", "0")
+    assert eng.conc_caps(1395256, True) is None
+    assert eng.conc_caps(88560, True) == (160, 96)
+    monkeypatch.setattr(eng, "_device_cus", lambda dev=None: 128)  # a partitioned device scales the split
+    monkeypatch.setattr(eng, "REW", "auto")
+    assert eng.conc_caps(1395256, True) == (64, 64)
+    assert eng.conc_caps(44280, True) == (80, 48)
+    monkeypatch.setattr(eng, "CONC_WGRAD", "0")
+    assert eng.conc_caps(88560, True) is None
+    monkeypatch.setattr(eng, "CONC_WGRAD", "168,88")
+    assert eng.conc_caps(11070, False) == (168, 88)
