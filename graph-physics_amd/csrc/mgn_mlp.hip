@@ -173,6 +173,9 @@ struct Gemm {
 // exposed one L2 round trip per 8 k-steps: measured, MGN_STAMPS, fp32 h=32 edge forward: 19.4k of
 // 38k cycles in the GEMMs of layers 0-2). WlDesc: per layer, source element offset in the pack and
 // element count; LDS copies are consecutive (layer l at wl_lo[l] elements).
+#ifndef MGN_WL_BATCH
+#define MGN_WL_BATCH 1  // A/B builds: 0 = the descriptor read field by field inside the layer loop
+#endif
 struct WlDesc {
     int32_t n;                      // layers staged (0: weights read from global memory)
     int32_t pad;
@@ -183,18 +186,30 @@ struct WlDesc {
 
 // issue the LDS-DMA copies (all waves; 16 bytes per lane, a wave instruction = 1 KiB); the caller
 // waits vmcnt(0) and barriers before the first read
+// The descriptor is copied whole (one batch of scalar loads) and the layer loop unrolled: a loop
+// over d.n re-read d.cnt / d.src / d.lo from the kernel arguments layer by layer, one scalar-load
+// round trip each before the layer's copies could issue (MGN_STAMPS: 4.3-5.6k cycles to issue the
+// copies of a 4-layer MLP, ahead of every generic launch's first input load).
 template <class T>
 __device__ __forceinline__ void wl_issue(const WlDesc& d, const T* pack, T* lds) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     constexpr int EPL = 16 / sizeof(T);  // elements per lane
-    for (int l = 0; l < d.n; ++l) {
-        const int pieces = (d.cnt[l] + 64 * EPL - 1) / (64 * EPL);
+#if MGN_WL_BATCH
+    const WlDesc w = d;
+#else
+    const WlDesc& w = d;
+#endif
+#pragma unroll
+    for (int l = 0; l < MGN_MAX_LAYERS; ++l) {
+        if (l >= w.n) break;
+        const int pieces = (w.cnt[l] + 64 * EPL - 1) / (64 * EPL);
         for (int pc = wave; pc < pieces; pc += nw) {
             const int e0 = pc * 64 * EPL;
-            if (e0 + lane * EPL < d.cnt[l])
+            if (e0 + lane * EPL < w.cnt[l])
                 __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(pack + d.src[l] + e0 + lane * EPL),
-                    (__attribute__((address_space(3))) void*)(lds + d.lo[l] + e0), 16, 0, 0);
+                    (const __attribute__((address_space(1))) void*)(pack + w.src[l] + e0 + lane * EPL),
+                    (__attribute__((address_space(3))) void*)(lds + w.lo[l] + e0), 16, 0, 0);
         }
     }
 }
