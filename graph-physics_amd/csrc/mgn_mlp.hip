@@ -1470,6 +1470,25 @@ struct RgArgs {
     RgJob job[12];
 };
 
+#ifndef MGN_RG_JOBSCAN
+#define MGN_RG_JOBSCAN 1  // A/B builds: 0 = the job found by a while loop over the arguments
+#endif
+// The job of this workgroup: the last j with wg0_j <= blockIdx.x (wg0 increases with j). The loop
+// runs over the fixed-size array, unrolled, so every wg0's scalar load issues together; a while loop
+// paid one dependent scalar-load round trip per job passed.
+__device__ __forceinline__ int rg_job_index(const RgArgs& a) {
+    int jn = 0;
+#if MGN_RG_JOBSCAN
+    constexpr int NJ = (int)(sizeof(a.job) / sizeof(a.job[0]));
+#pragma unroll
+    for (int j = 1; j < NJ; ++j)
+        if (j < a.njobs && (int)blockIdx.x >= a.job[j].wg0) jn = j;
+#else
+    while (jn + 1 < a.njobs && (int)blockIdx.x >= a.job[jn + 1].wg0) ++jn;
+#endif
+    return jn;
+}
+
 // fp32 single-MLP job lists that mix 128-column jobs with narrower ones (A/B builds: 0 = all on the
 // generic kernel)
 #ifndef MGN_RING_SPLIT
@@ -1543,8 +1562,7 @@ __global__ __launch_bounds__(512) void wgrad_ring_kernel(RgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wn = w & 3, wk = w >> 2;
-    int jn = 0;
-    while (jn + 1 < a.njobs && (int)blockIdx.x >= a.job[jn + 1].wg0) ++jn;
+    const int jn = rg_job_index(a);
     const RgJob job = a.job[jn];
     const int chunk = (int)blockIdx.x - job.wg0;
     const int64_t r_begin = (int64_t)chunk * job.rows_per_chunk;
@@ -1695,8 +1713,7 @@ __global__ __launch_bounds__(512) void wgrad_ring_f32_kernel(RgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wn = w & 3, wk = w >> 2;
-    int jn = 0;
-    while (jn + 1 < a.njobs && (int)blockIdx.x >= a.job[jn + 1].wg0) ++jn;
+    const int jn = rg_job_index(a);
     const RgJob job = a.job[jn];
     const int chunk = (int)blockIdx.x - job.wg0;
     const int64_t r_begin = (int64_t)chunk * job.rows_per_chunk;
