@@ -1,7 +1,10 @@
 """bench.py — training-steps/sec of the MeshGraphNet hot path on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N --steps K --warmup W]
-    (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N)
+    N>1: `python bench.py --gpus N` starts its N ranks itself (torch.distributed.run as a child process,
+    before anything touches the GPU) and forwards rank 0's JSON line; run under a launcher
+    (python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N) it is
+    one of the launcher's ranks.
 
 Workload (BASELINE.json configs[1], SURVEY.md §8d Cfg B): CylinderFlow MeshGraphNet, 15 message-passing
 blocks, hidden 128, batch = 8 graphs per GPU (8 jittered copies of the reference's in-tree CylinderFlow
@@ -30,6 +33,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "graph-physics_amd")]
 
+OUT = sys.stdout  # the JSON line's stream (main() keeps the real stdout for it alone)
 METRIC = "training-steps/sec + one-step velocity MSE, CylinderFlow MGN 15MP h=128"
 PEAK = {"bf16": 2500.0, "fp32": 157.3}  # TFLOP/s dense (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0  # GB/s spec
@@ -65,6 +69,9 @@ def parse():
                          "plate: Cfg C (DeformingPlate-shaped tet mesh + world edges)")
     ap.add_argument("--print-workload", action="store_true",
                     help="print the workload key the PMC files are stamped with, and exit")
+    ap.add_argument("--dry", action="store_true",
+                    help="launcher check: start the ranks, form the process group (gloo), agree on the world "
+                         "size, print the JSON line's rank/world fields and exit before any GPU call")
     a = ap.parse_args()
     if a.fresh_batch:
         a.no_graph = True
@@ -385,16 +392,86 @@ def secondary(a0, dev, mesh, label, cpu_steps=0, **over):
     return r
 
 
+def launch_ranks(a):
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher: start the N ranks as ONE
+    child process — torch.distributed.run on this script with the same arguments, one rank per GPU of
+    this node, rendezvous on 127.0.0.1 — before this process touches the GPU (no exec: the parent only
+    waits). The children's stderr passes through; their stdout (rank 0's single JSON line) is forwarded.
+    Returns the child's exit status (non-zero if any rank failed)."""
+    import socket
+    import subprocess
+
+    backend = os.environ.get("MGN_DIST_BACKEND", "nccl")
+    if backend == "nccl" and not a.dry:
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+        if ndev < a.gpus:
+            print("bench.py: --gpus %d but %d GPU(s) visible (one RCCL rank per GPU; MGN_DIST_BACKEND=gloo "
+                  "rehearses several ranks per GPU)" % (a.gpus, ndev), file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % a.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MGN_BENCH_LAUNCHED="%d" % a.gpus)
+    print("[bench] starting %d ranks: %s" % (a.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    for line in p.stdout:
+        if line.startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def dry_run(a, rank, world):
+    """--dry: the process group of the launched ranks (gloo, no device), every rank's (rank, world) agreed
+    by an all_gather; rank 0 prints the fields the bench line would carry."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        import socket
+
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = torch.tensor([rank, world], dtype=torch.int64)
+    allv = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    ranks = sorted(int(t[0]) for t in allv)
+    if ranks != list(range(world)) or any(int(t[1]) != world for t in allv):
+        raise RuntimeError("ranks disagree on the world: %s" % [t.tolist() for t in allv])
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry": True, "n_gpus": world, "ranks": ranks,
+                          "launched_by": "bench.py" if os.environ.get("MGN_BENCH_LAUNCHED") else "external",
+                          "config": {"parallelism": "dp%d" % world}}), file=OUT, flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     a = parse()
     if a.print_workload:
         print(workload_key(a))
         return
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    # the JSON line is the only thing on stdout: everything else written to file descriptor 1 (gloo's
+    # "[Gloo] Rank ... connected" lines, library prints) goes to stderr
+    global OUT
+    sys.stdout.flush()
+    OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != a.gpus:
+        print("[bench rank %d] --gpus %d under a launcher of %d rank(s): measuring %d" % (rank, a.gpus, world, world),
+              file=sys.stderr, flush=True)
         a.gpus = world
+    if a.dry:
+        dry_run(a, rank, world)
+        return
     # MGN_DIST_BACKEND=gloo (rehearsal only): several ranks share the visible GPUs round-robin and
     # exchange through host memory; the default "nccl" is RCCL over xGMI, one rank per GPU
     backend = os.environ.get("MGN_DIST_BACKEND", "nccl")
@@ -571,7 +648,7 @@ def main():
                                          "N=22,535, E=1,395,256), MP=15, h=128, bf16", dtype="bf16", mp=15,
                                          hidden=128, batch=1, workload="aneurysm")
         out["secondary"] = sec
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=OUT, flush=True)
     if world > 1:
         dist.barrier()
     if dist.is_initialized():

@@ -42,6 +42,8 @@ struct ChainRewArgs {
     float* part;                // slab c at part + c * G
     int64_t G;
     int64_t w_off[4], b_off[4]; // layer l's weight / bias offsets in a slab
+    uint32_t* err;              // device error word (mgn_call_opts; may be NULL): MGN_ERR_HANDOFF on a timeout
+    uint32_t spin;              // polls per hand-off wait before it gives up
 };
 
 struct ChainBwdArgs {

@@ -190,19 +190,34 @@ __host__ __device__ __forceinline__ int64_t r8_index(int64_t m, int64_t c, int64
 // CUs the persistent kernels size their grids for. MGN_MAX_CUS (read once) caps it, so two streams
 // can each run a persistent kernel on part of the chip at the same time (intra-GPU data parallelism
 // experiments: tools/exp_dual.py).
-// Runtime caps (mgn_set_grid_cus, ABI v13; 0 = none): the persistent grids of every launch except
-// the weight-gradient launches (g_cap_data), and of the weight-gradient launches (g_cap_wgrad), so a
-// block's weight gradients can run on a stream of their own beside the next block's data gradients,
-// each on its own share of the CUs. Read when a launch is issued (a captured graph keeps its grids).
-extern int g_cap_data, g_cap_wgrad;
+// Per-call options (mgn_call_opts, ABI v17; replaces v13's process-global mgn_set_grid_cus): the CU
+// caps of the persistent grids of every launch except the weight-gradient launches (data_cus) and of
+// the weight-gradient launches (wgrad_cus; 0 = none), so a block's weight gradients can run on a stream
+// of their own beside the next block's data gradients, each on its own share of the CUs; and the device
+// error word the hand-off waits of the recomputed weight gradients report a timeout to. CallScope
+// installs a call's options for the duration of that call only, on the calling thread (restored on
+// return), so two models, streams or threads never see each other's caps. Read when a launch is issued
+// (a captured graph keeps its grids).
+struct MgnCallCtx {
+    int data_cus, wgrad_cus;
+    uint32_t* err_word;
+};
+extern thread_local MgnCallCtx g_call;
+struct CallScope {
+    MgnCallCtx saved;
+    explicit CallScope(const mgn_call_opts* o) : saved(g_call) {
+        g_call = MgnCallCtx{o ? o->data_cus : 0, o ? o->wgrad_cus : 0, o ? o->err_word : nullptr};
+    }
+    ~CallScope() { g_call = saved; }
+};
 inline int hw_cus();
 inline int device_cus() {
     const int c = hw_cus();
-    return g_cap_data > 0 && g_cap_data < c ? g_cap_data : c;
+    return g_call.data_cus > 0 && g_call.data_cus < c ? g_call.data_cus : c;
 }
 inline int wgrad_cus() {
     const int c = hw_cus();
-    return g_cap_wgrad > 0 && g_cap_wgrad < c ? g_cap_wgrad : c;
+    return g_call.wgrad_cus > 0 && g_call.wgrad_cus < c ? g_call.wgrad_cus : c;
 }
 inline int hw_cus() {
     static int cus = 0;

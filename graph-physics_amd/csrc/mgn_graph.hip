@@ -15,7 +15,7 @@
 
 #include "mgn_common.h"
 
-int g_cap_data = 0, g_cap_wgrad = 0;  // mgn_set_grid_cus
+thread_local MgnCallCtx g_call = {0, 0, nullptr};  // CallScope (mgn_call_opts, ABI v17)
 
 static thread_local std::string g_err;
 void mgn_set_error(const std::string& s) { g_err = s; }
@@ -554,12 +554,6 @@ int mgn_adamw_dev(float* param, const float* grad, float* exp_avg, float* exp_av
 }
 
 int mgn_abi_version(void) { return MGN_ABI_VERSION; }
-int mgn_set_grid_cus(int32_t data_cus, int32_t wgrad_cus) {
-    MGN_REQUIRE(data_cus >= 0 && wgrad_cus >= 0, "CU caps must be >= 0 (0 = no cap)");
-    g_cap_data = data_cus;
-    g_cap_wgrad = wgrad_cus;
-    return 0;
-}
 const char* mgn_last_error(void) { return g_err.c_str(); }
 
 size_t mgn_topology_workspace_bytes(int64_t E, int64_t N) {

@@ -3109,10 +3109,14 @@ int64_t rew_max_chunks(int64_t RP) {
     if (c > cap) c = cap;
     return c < 1 ? 1 : c;
 }
+// Only an edge MLP of a chained bf16 h=128 block (layer-0 input [e ‖ x_i ‖ x_j] = 3h columns) can run
+// the recompute, so only its slab capacity is raised (node MLPs never need it), and never
+// beyond one slab per CU (the recompute launch runs at most wgrad_cus() chunks)
 int64_t slab_chunks(int64_t RP, const mgn_mlp* m) {
     const int64_t c = wgrad_max_chunks(RP, m->hidden);
-    if (m->hidden != 128 || m->dtype != MGN_BF16) return c;
-    const int64_t r = rew_max_chunks(RP);
+    if (m->hidden != 128 || m->dtype != MGN_BF16 || m->in_dim != 3 * m->hidden) return c;
+    int64_t r = rew_max_chunks(RP);
+    if (r > hw_cus()) r = hw_cus();
     return r > c ? r : c;
 }
 int wgrad_rows_per_chunk(int64_t RP, int njobs, int H = 128) {
@@ -4260,6 +4264,17 @@ int mgn_mlp_backward_deferred2(const mgn_mlp* m, const void* in, int32_t in_dtyp
     return 0;
 }
 
+int mgn_mlp_backward_deferred3(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                               const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved, const void* dout,
+                               int32_t dout_dtype, void* din, int32_t din_dtype, float* grads, void* ws,
+                               size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce1,
+                               int32_t flags, const mgn_call_opts* opts, mgn_stream_t stream) {
+    MGN_REQUIRE(!opts || (opts->data_cus >= 0 && opts->wgrad_cus >= 0), "CU caps must be >= 0 (0 = no cap)");
+    CallScope cs(opts);
+    return mgn_mlp_backward_deferred2(m, in, in_dtype, in_ld, in_rows, rows, saved, dout, dout_dtype, din, din_dtype,
+                                      grads, ws, ws_bytes, keep, keep_bytes, reduce1, flags, stream);
+}
+
 static size_t block_fwd_ws(const mgn_topology* t, const mgn_mlp* edge) {
     return align_up((size_t)t->num_nodes * 2 * edge->hidden * sizeof(float));
 }
@@ -4790,6 +4805,17 @@ int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, con
         return r;
     memcpy(reduce2, d, sizeof(d));
     return 0;
+}
+
+int mgn_block_backward_deferred3(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                                 const void* e, const mgn_block_saved* saved, const void* dx_out, const void* de_out,
+                                 void* dx, void* de, float* edge_grads, float* node_grads, void* ws,
+                                 size_t ws_bytes, void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
+                                 int32_t flags, const mgn_call_opts* opts, mgn_stream_t stream) {
+    MGN_REQUIRE(!opts || (opts->data_cus >= 0 && opts->wgrad_cus >= 0), "CU caps must be >= 0 (0 = no cap)");
+    CallScope cs(opts);
+    return mgn_block_backward_deferred2(t, edge, node, x, e, saved, dx_out, de_out, dx, de, edge_grads, node_grads, ws,
+                                        ws_bytes, keep, keep_bytes, reduce2, flags, stream);
 }
 
 int mgn_wgrad_reduce_many(const mgn_wgrad_reduce* reds, int32_t n, mgn_stream_t stream) {

@@ -32,8 +32,14 @@ constexpr int REW_IMG = REW_SR * H * 2;      // one 32-row bf16 image (8 KiB)
 constexpr size_t REW_LDS_W = (size_t)3 * LFR * FRAG * 2;  // layers 0..2 (96 KiB)
 static_assert((REW_LDS_W + 4 * H * 4) % 256 == 0 && REW_IMG % 256 == 0, "images on 256-byte boundaries (rew_get_tr's XOR)");
 constexpr size_t REW_LDS = REW_LDS_W + 4 * H * 4 + (size_t)6 * REW_IMG + 4 * REW_FLAGS;
+// Bounded hand-off waits: MGN_REW_SPIN polls (s_sleep 1 each, ~0.5 s at 2.4 GHz) before a wait gives
+// up — a correct pipeline never comes near. The environment variable of the same name overrides it
+// (diagnostics: MGN_REW_SPIN=0 makes every wait fail, tests/test_step_gpu.py). A wait that gives up
+// ends its wave's loop (every wave still reaches the end of the kernel: the waits it would have served
+// give up in turn), ORs MGN_ERR_HANDOFF into the call's error word and makes the workgroup's slab
+// regions NaN instead of partial sums, so a timeout can never become a silently wrong gradient.
 #ifndef MGN_REW_SPIN
-#define MGN_REW_SPIN (1u << 24)  // bounded hand-off waits (a correct pipeline never comes near)
+#define MGN_REW_SPIN (1u << 24)
 #endif
 
 __device__ __forceinline__ int rew_slot(int r, int ch) { return r * (H * 2) + 16 * (ch ^ ((((r & 3) << 2) | ((r >> 2) & 3)))); }
@@ -103,8 +109,8 @@ __device__ __forceinline__ void gemm16_k2(f4 (&acc)[8], const __bf16* W, int l, 
 // in order, so "image stores; s_waitcnt lgkmcnt(0); counter store" publishes the image, and the reader's
 // counter load completes before its image loads issue. (A release / acquire at workgroup scope would
 // also wait for the wave's outstanding global loads — the next step's prefetch — at every hand-off.)
-__device__ __forceinline__ bool rew_wait(const unsigned* f, unsigned target) {
-    for (unsigned n = 0; n < MGN_REW_SPIN; ++n) {
+__device__ __forceinline__ bool rew_wait(const unsigned* f, unsigned target, unsigned spin) {
+    for (unsigned n = 0; n < spin; ++n) {
         if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             return true;
@@ -112,6 +118,10 @@ __device__ __forceinline__ bool rew_wait(const unsigned* f, unsigned target) {
         __builtin_amdgcn_s_sleep(1);
     }
     return false;
+}
+// a wait gave up: report it on the call's device error word (a vector atomic from one lane)
+__device__ __forceinline__ void rew_fail(const ChainRewArgs& a, int lane) {
+    if (lane == 0 && a.err != nullptr) atomicOr(a.err, (unsigned)MGN_ERR_HANDOFF);
 }
 __device__ __forceinline__ void rew_signal(unsigned* f, unsigned v, int lane) {
     lds_fence();
@@ -172,8 +182,8 @@ __global__ __launch_bounds__(REW_WAVES * 64, 1) void chain16_rew_kernel(ChainRew
         // ---- producers: image i, tile u (16 rows) of every 32-row step
         const int i = wave >> 1, u = wave & 1;
         auto slot_free = [&](int s) -> bool {
-            if (!rew_wait(FD + 2 * i, prev(s)) || !rew_wait(FD + 2 * i + 1, prev(s))) return false;
-            return i == 2 || rew_wait(FC + 2 * i + u, prev(s));
+            if (!rew_wait(FD + 2 * i, prev(s), a.spin) || !rew_wait(FD + 2 * i + 1, prev(s), a.spin)) return false;
+            return i == 2 || rew_wait(FC + 2 * i + u, prev(s), a.spin);
         };
         if (i == 0) {
             // layer 0 (chain16_fwd_kernel's operations: e·W0a, + P_i + P_j, ReLU). A step's operands
@@ -236,13 +246,21 @@ __global__ __launch_bounds__(REW_WAVES * 64, 1) void chain16_rew_kernel(ChainRew
                 return true;
             };
             int s = 0;
+            bool ok = true;
             for (; s + 1 < nsteps; s += 2)
-                if (!step(s, eb, ebn) || !step(s + 1, ebn, eb)) break;
-            if (s + 1 == nsteps) step(s, eb, ebn);
+                if (!step(s, eb, ebn) || !step(s + 1, ebn, eb)) {
+                    ok = false;
+                    break;
+                }
+            if (ok && s + 1 == nsteps) ok = step(s, eb, ebn);
+            if (!ok) rew_fail(a, lane);
         } else {
             // layer i on X_i (tile u of image i - 1): + b_i, ReLU -> X_{i+1}
             for (int s = 0; s < nsteps; ++s) {
-                if (!rew_wait(RD + 2 * (i - 1) + u, (unsigned)(s + 1))) break;
+                if (!rew_wait(RD + 2 * (i - 1) + u, (unsigned)(s + 1), a.spin)) {
+                    rew_fail(a, lane);
+                    break;
+                }
                 RS(0);
                 bf16x8 X[4];
                 rew_get_op(img(i - 1, s), X, u, lane);
@@ -254,7 +272,10 @@ __global__ __launch_bounds__(REW_WAVES * 64, 1) void chain16_rew_kernel(ChainRew
 #pragma unroll
                     for (int r = 0; r < 4; ++r) x[t][r] = fmaxf(x[t][r], 0.f);
                 RS(1);
-                if (!slot_free(s)) break;
+                if (!slot_free(s)) {
+                    rew_fail(a, lane);
+                    break;
+                }
                 rew_put<8>(img(i, s), x, u, 0, lane);
                 rew_signal(RD + 2 * i + u, (unsigned)(s + 1), lane);
                 RS(2);
@@ -288,9 +309,13 @@ __global__ __launch_bounds__(REW_WAVES * 64, 1) void chain16_rew_kernel(ChainRew
     uint32_t tlo, thi;
     rew_tr_base(lane, tlo, thi);
     if (nsteps > 0) loadA(0);
+    bool ok = true;
     for (int s = 0; s < nsteps; ++s) {
-        if (!rew_wait(RD + 2 * (l - 1), (unsigned)(s + 1)) || !rew_wait(RD + 2 * (l - 1) + 1, (unsigned)(s + 1)))
+        if (!rew_wait(RD + 2 * (l - 1), (unsigned)(s + 1), a.spin) ||
+            !rew_wait(RD + 2 * (l - 1) + 1, (unsigned)(s + 1), a.spin)) {
+            ok = false;
             break;
+        }
         RS(0);
         // db first: A is then dead after the MFMAs and the next step's loads land in its registers
 #pragma unroll
@@ -318,7 +343,18 @@ __global__ __launch_bounds__(REW_WAVES * 64, 1) void chain16_rew_kernel(ChainRew
     }
     // this wave's rows of layer l's slab regions: dW [128][128] and db. The MFMAs computed dWᵀ tiles
     // (X fragments as the row operand): lane (m, g) holds dW[64hf + 16nt + m][16kt + 4g .. + 3], one
-    // 16-byte store
+    // 16-byte store. A timed-out wait (here or in a producer wave, whose failure makes this wave's waits
+    // time out in turn) stores NaN, never the partial sums
+    if (!ok) {
+        rew_fail(a, lane);
+        const float nan = __builtin_nanf("");
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            bs[nt] = nan;
+#pragma unroll
+            for (int kt = 0; kt < 8; ++kt) acc[nt][kt] = f4{nan, nan, nan, nan};
+        }
+    }
     float* slab = a.part + (int64_t)blockIdx.x * a.G;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -358,6 +394,9 @@ int chain16_edge_wgrad_recompute(const mgn_mlp* m, const void* e, const void* pr
     a.nchunks = nchunks;
     a.part = part;
     a.G = G;
+    a.err = g_call.err_word;
+    a.spin = MGN_REW_SPIN;
+    if (const char* v = getenv("MGN_REW_SPIN")) a.spin = (uint32_t)strtoul(v, nullptr, 0);
     int64_t o = 0;
     for (int l = 0; l < 4; ++l) {
         int n, k;

@@ -10,7 +10,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmgn.so")
-ABI_VERSION = 16  # include/mgn.h MGN_ABI_VERSION these bindings are written for
+ABI_VERSION = 17  # include/mgn.h MGN_ABI_VERSION these bindings are written for
 
 MGN_F32 = 0
 MGN_BF16 = 1
@@ -54,6 +54,11 @@ class WgradReduce(ctypes.Structure):
     _fields_ = [("part", _vp), ("dsp", _vp), ("grads", _vp), ("G", _i64), ("nchunks", _i32), ("ntiles", _i32),
                 ("NS", _i32), ("blocks", _i32), ("w0_n", _i32), ("w0_k", _i32), ("xcol0", _i32), ("nchunks_x", _i32),
                 ("hoff", _i64), ("nchunks_h", _i32), ("pad", _i32)]
+
+
+class CallOpts(ctypes.Structure):
+    """mgn_call_opts (ABI v17): per-call CU caps and the device error word (mgn.h)."""
+    _fields_ = [("data_cus", _i32), ("wgrad_cus", _i32), ("err_word", _vp)]
 
 
 class NormalizerState(ctypes.Structure):
@@ -115,7 +120,13 @@ EXPORTS = {
                                             _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
                                             _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _i32, _vp]),
     "mgn_wgrad_reduce_many": (_i32, [ctypes.POINTER(WgradReduce), _i32, _vp]),
-    "mgn_set_grid_cus": (_i32, [_i32, _i32]),
+    "mgn_block_backward_deferred3": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                            _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _sz, _vp, _sz, ctypes.POINTER(WgradReduce), _i32,
+                                            ctypes.POINTER(CallOpts), _vp]),
+    "mgn_mlp_backward_deferred3": (_i32, [ctypes.POINTER(Mlp), _vp, _i32, _i64, _vp, _i64,
+                                          ctypes.POINTER(MlpSaved), _vp, _i32, _vp, _i32, _vp, _vp, _sz, _vp, _sz,
+                                          ctypes.POINTER(WgradReduce), _i32, ctypes.POINTER(CallOpts), _vp]),
     "mgn_debug_wave_times": (_i32, [_i32, _vp, _i32]),
     "mgn_permute_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "mgn_segment_sum": (_i32, [_vp, _vp, _i64, _i32, _i32, _vp, _vp]),
@@ -207,6 +218,7 @@ def check(rc):
 
 # ---------------------------------------------------------------- device error word (ABI v7)
 ERR_EDGE_INDEX, ERR_TYPE_NEG, ERR_TYPE_BIG = 1, 2, 4
+ERR_HANDOFF = 8  # ABI v17: a pipelined kernel's bounded hand-off wait timed out (mgn.h MGN_ERR_HANDOFF)
 ERR_ANY, ERR_SKIP_SHIFT, ERR_STALE = 0xFFFF, 16, 1 << 31  # ABI v11 (include/mgn.h)
 
 
@@ -222,6 +234,11 @@ def _raise_for(bits):
         ex = RuntimeError("Class values must be non-negative.")  # F.one_hot (reference simulator one-hot)
     elif bits & ERR_TYPE_BIG:
         ex = RuntimeError("Class values must be smaller than num_classes.")
+    elif bits & ERR_HANDOFF:
+        # not a validation error of the batch: a libmgn kernel (the recomputed edge weight gradients)
+        # gave up waiting inside its pipeline and wrote NaN partial sums; the optimizer step was skipped
+        ex = RuntimeError("libmgn: a hand-off wait of the recomputed weight gradients timed out "
+                          "(MGN_ERR_HANDOFF); the step's gradients are invalid and its optimizer update was skipped")
     if ex is not None:
         ex.mgn_skipped_updates = (bits >> ERR_SKIP_SHIFT) & 0xFF
         raise ex

@@ -100,7 +100,7 @@ GRAD_GROUP_BYTES = 4 << 20
 PAIR_DE = os.environ.get("MGN_PAIR_DE", "1") == "1"
 # Processor backward with each block's weight-gradient launch on a side stream, beside the next
 # block's data-gradient kernels (mgn_block_backward_deferred2 MGN_BWD_DATA_ONLY / _WGRAD_ONLY, two
-# workspaces), each on its own share of the CUs (mgn_set_grid_cus). MGN_CONC_WGRAD: "auto" (default:
+# workspaces), each on its own share of the CUs (per-call mgn_call_opts caps, ABI v17). MGN_CONC_WGRAD: "auto" (default:
 # conc_caps below), "0" (one stream), or "data_cus,wgrad_cus" (0,0: both streams uncapped).
 CONC_WGRAD = os.environ.get("MGN_CONC_WGRAD", "auto")
 # concurrent backward: workspaces rotated between blocks (MGN_CONC_WS = count or "all" = one per block).
@@ -459,11 +459,13 @@ def _empty(n, dtype, device):
     return torch.empty(max(int(n), 1), dtype=dtype, device=device)
 
 
-def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
+def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False, with_act=True):
+    """with_act False: the R8 layer inputs are never written (the recomputed edge weight gradients) — a
+    one-element placeholder (non-NULL: the training forward's kernels) instead of the full buffer."""
     ae, mw = ctypes.c_int64(), ctypes.c_int64()
     nat.check(nat.lib().mgn_mlp_saved_elems(ctypes.byref(desc), rows, int(block_mlp), ctypes.byref(ae),
                                             ctypes.byref(mw)))
-    act = _empty(ae.value, tdt, device)
+    act = _empty(ae.value if with_act else 1, tdt, device)
     mask = _empty(mw.value, torch.int64, device)
     z = _empty(rows * spec.width, tdt, device) if need_z else None
     rden = _empty(rows, torch.float32, device) if need_z else None
@@ -475,10 +477,7 @@ def _alloc_mlp_saved(desc, spec, rows, tdt, device, need_z, block_mlp=False):
 def _alloc_block_saved(edesc, ndesc, espec, nspec, topo, tdt, device, edge_act=True):
     """edge_act False (mgn_block_saved.proj): the edge MLP's R8 inputs are never written — a
     one-element placeholder (non-NULL: the training forward's kernels)."""
-    se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True, True)
-    if not edge_act:
-        ke = (_empty(1, tdt, device),) + tuple(ke[1:])
-        se.act = ke[0].data_ptr()
+    se, ke = _alloc_mlp_saved(edesc, espec, topo.num_edges, tdt, device, True, True, with_act=edge_act)
     sn, kn = _alloc_mlp_saved(ndesc, nspec, topo.num_nodes, tdt, device, nspec.norm is not None, True)
     aggr = _empty(topo.num_nodes * espec.width, tdt, device)
     return nat.BlockSaved(se, sn, aggr.data_ptr()), (ke, kn, aggr)
@@ -520,22 +519,21 @@ def _mlp_bwd(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, di
 
 
 def _mlp_bwd_deferred(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws,
-                      keep, red, stream):
-    """_mlp_bwd with the reduction left to one mgn_wgrad_reduce_many at the end of the backward."""
-    nat.check(nat.lib().mgn_mlp_backward_deferred(
-        ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld, nat.ptr(rows_idx), rows, ctypes.byref(saved),
-        nat.ptr(dout), dout_mdt, nat.ptr(din), din_mdt, nat.ptr(grads), nat.ptr(ws), ws.numel(), nat.ptr(keep),
-        keep.numel(), red, stream))
+                      keep, red, stream, opts=None):
+    """_mlp_bwd with the reduction left to one mgn_wgrad_reduce_many at the end of the backward; opts: the
+    call's mgn_call_opts (CU caps, error word; ABI v17)."""
+    _mlp_bwd_half(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws, keep,
+                  red, 0, stream, opts)
 
 
 def _mlp_bwd_half(desc, inp, in_mdt, in_ld, rows_idx, rows, saved, dout, dout_mdt, din, din_mdt, grads, ws, keep,
-                  red, flags, stream):
-    """One half of _mlp_bwd_deferred (mgn_mlp_backward_deferred2, ABI v14): flags MGN_BWD_DATA_ONLY, then
-    MGN_BWD_WGRAD_ONLY with the same arguments (red carries the partial-row count between them)."""
-    nat.check(nat.lib().mgn_mlp_backward_deferred2(
+                  red, flags, stream, opts=None):
+    """One half of _mlp_bwd_deferred (mgn_mlp_backward_deferred3, ABI v17): flags MGN_BWD_DATA_ONLY, then
+    MGN_BWD_WGRAD_ONLY with the same arguments (red carries the partial-row count between them); 0: whole."""
+    nat.check(nat.lib().mgn_mlp_backward_deferred3(
         ctypes.byref(desc), nat.ptr(inp), in_mdt, in_ld, nat.ptr(rows_idx), rows, ctypes.byref(saved),
         nat.ptr(dout), dout_mdt, nat.ptr(din), din_mdt, nat.ptr(grads), nat.ptr(ws), ws.numel(), nat.ptr(keep),
-        keep.numel(), red, flags, stream))
+        keep.numel(), red, flags, ctypes.byref(opts) if opts is not None else None, stream))
 
 
 def _mlp_keep(desc, rows, dev):
@@ -630,9 +628,8 @@ class EPDFunction(torch.autograd.Function):
             x1 = torch.empty((N, H), dtype=tdt, device=dev)
             e1 = torch.empty((E, H), dtype=tdt, device=dev)
             fws, nws = (fwss[b], fwss[min(b + 1, nb - 1)]) if rew else (fwss[b % 2], fwss[(b + 1) % 2])
-            if rew:
+            if rew:  # the block's projections stay alive for its backward (ctx.state), outside sv[1]
                 sv[0].proj = fws.data_ptr()
-                sv = (sv[0], sv[1] + (fws,))
             nxt = ctypes.byref(bdescs[2 * b + 2]) if CHAIN_PROJ and b + 1 < nb else None
             proj_ready = ready.value
             nat.check(nat.lib().mgn_block_forward_chain(
@@ -655,12 +652,14 @@ class EPDFunction(torch.autograd.Function):
             if dec.out_width != dec.out_dim:  # a decoder whose output width is the (padded) hidden size
                 out = out[:, :dec.out_dim].contiguous()
         if train and INSPECT is not None:
+            # rew: the edge MLPs' R8 inputs were not saved (sv[1][0][0] is a placeholder)
             INSPECT(dict(topo=topo, plan=plan, mdt=mdt, only_processor=only_processor, svs=svs, sv_ne=sv_ne,
-                         sv_ee=sv_ee, sv_dec=sv_dec))
+                         sv_ee=sv_ee, sv_dec=sv_dec, rew=rew))
         if train:
             ctx.plan, ctx.mdt, ctx.only_processor, ctx.topo = plan, mdt, only_processor, topo
             ctx.pw = pw
             ctx.state = (xin, ein, xs, es, svs, sv_ne, sv_ee, sv_dec)
+            ctx.fwss = fwss if rew else None  # rew: per-block node projections read by the backward
             ctx.H = H
         return out
 
@@ -713,6 +712,13 @@ class EPDFunction(torch.autograd.Function):
         early_dec = defer_dense and GRAD_READY is not None
         LAST_SCHEDULE.update(conc=caps if conc else None, side_reduced=side_reduced, defer_dense=defer_dense,
                              early_dec=early_dec, grad_ready=GRAD_READY is not None)
+        # per-call options (ABI v17): CU caps of the concurrent section's launches, and the device error word
+        # the recomputed weight gradients report a hand-off timeout on (the step's AdamW is then skipped and
+        # the next poll raises)
+        ew = nat.error_word(dev)
+        opts0 = nat.CallOpts(0, 0, ew.ptr().value)
+        optsc = nat.CallOpts(caps[0], caps[1], ew.ptr().value) if conc else opts0
+        optse = nat.CallOpts(caps[0], caps[0] if ENC_DATA_CAP else caps[1], ew.ptr().value) if conc else opts0
         need = _ws_bytes_block(topo, bdescs[0], bdescs[1]) if len(bdescs) >= 2 else 0
         if not ctx.only_processor:
             need = max(need, _ws_bytes_mlp(descs[0], N), _ws_bytes_mlp(descs[1], E),
@@ -725,10 +731,10 @@ class EPDFunction(torch.autograd.Function):
         side = _side_stream(dev) if (conc or overlap) else None
         dec_args = None
 
-        def dec_wgrad(stream):
+        def dec_wgrad(stream, opts):
             """The decoder's weight-gradient half on `stream` (early_dec: reduced and handed over there)."""
             sp = nat._vp(stream.cuda_stream)
-            _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, sp)
+            _mlp_bwd_half(*dec_args, nat.MGN_BWD_WGRAD_ONLY, sp, opts)
             if early_dec:
                 nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(dreds[0]), 1, sp))
                 with torch.cuda.stream(stream):
@@ -745,9 +751,9 @@ class EPDFunction(torch.autograd.Function):
                 wsd = torch.empty(max(_ws_bytes_mlp(descs[2], N), 1), dtype=torch.uint8, device=dev)
                 dec_args = (descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
                             ctypes.c_void_p(gp + 4 * off[2]), wsd, keeps[0], ctypes.pointer(dreds[0]))
-                _mlp_bwd_half(*dec_args, nat.MGN_BWD_DATA_ONLY, st)
+                _mlp_bwd_half(*dec_args, nat.MGN_BWD_DATA_ONLY, st, opts0)
                 if not (DEC_SPLIT and conc):  # weight gradients at once, on the whole chip
-                    dec_wgrad(main)
+                    dec_wgrad(main, opts0)
                     dec_args = None
             else:
                 _mlp_bwd(descs[2], xs[-1], mdt, H, None, N, sv_dec[0], g, nat.MGN_F32, dx, mdt,
@@ -775,153 +781,144 @@ class EPDFunction(torch.autograd.Function):
             nws = nb if CONC_WS == "all" else max(int(CONC_WS), 2)
             wss = [torch.empty_like(ws) for _ in range(nws)]
             done = [None] * nws
-            # process-global CU caps of libmgn's launches: reset in the finally below, so an error
-            # anywhere in the concurrent section never leaves later launches capped
-            nat.check(L.mgn_set_grid_cus(*caps))
-        try:
-            if dec_args is not None:  # the decoder's weight gradients on the side stream, beside block nb-1's
-                ev = torch.cuda.Event()  # data half
+        if dec_args is not None:  # the decoder's weight gradients on the side stream, beside block nb-1's
+            ev = torch.cuda.Event()  # data half
+            ev.record(main)
+            side.wait_event(ev)
+            dec_wgrad(side, optsc)
+        for b in reversed(range(nb)):
+            dx1 = torch.empty((N, H), dtype=tdt, device=dev)
+            de1 = torch.empty((E, H), dtype=tdt, device=dev)
+            args = (ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
+                    nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
+                    nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
+                    ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
+            blo = boff[2 * b]
+            bhi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
+            # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
+            # layout); the first block's stay row-major (the encoders / the caller read them)
+            flags = 0
+            if pair_de:
+                if b + 1 < nb:
+                    flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
+                if b > 0:
+                    flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
+            if conc:
+                w = wss[b % nws]
+                if done[b % nws] is not None:
+                    main.wait_event(done[b % nws])  # the side stream is done reading this workspace
+                kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
+                nat.check(L.mgn_block_backward_deferred3(*args, nat.ptr(w), w.numel(), kp, kb,
+                                                         ctypes.pointer(reds[2 * b]),
+                                                         flags | nat.MGN_BWD_DATA_ONLY, ctypes.byref(optsc), st))
+                ev = torch.cuda.Event()
                 ev.record(main)
                 side.wait_event(ev)
-                dec_wgrad(side)
-            for b in reversed(range(nb)):
-                dx1 = torch.empty((N, H), dtype=tdt, device=dev)
-                de1 = torch.empty((E, H), dtype=tdt, device=dev)
-                args = (ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
-                        nat.ptr(xs[b]), nat.ptr(es[b]), ctypes.byref(svs[b][0]), nat.ptr(dx), nat.ptr(de),
-                        nat.ptr(dx1), nat.ptr(de1), ctypes.c_void_p(gp + 4 * boff[2 * b]),
-                        ctypes.c_void_p(gp + 4 * boff[2 * b + 1]))
-                blo = boff[2 * b]
-                bhi = boff[2 * b + 1] + bspecs_numel(plan, ctx.only_processor, 2 * b + 1)
-                # de / dx between consecutive blocks in the pair layout (the chained kernels' gather
-                # layout); the first block's stay row-major (the encoders / the caller read them)
-                flags = 0
-                if pair_de:
-                    if b + 1 < nb:
-                        flags |= nat.MGN_BWD_DE_OUT_PAIR | nat.MGN_BWD_DX_OUT_PAIR
-                    if b > 0:
-                        flags |= nat.MGN_BWD_DE_PAIR | nat.MGN_BWD_DX_PAIR
-                if conc:
-                    w = wss[b % nws]
-                    if done[b % nws] is not None:
-                        main.wait_event(done[b % nws])  # the side stream is done reading this workspace
-                    kp = ctypes.c_void_p(keep.data_ptr() + b * kb)
-                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb,
-                                                             ctypes.pointer(reds[2 * b]),
-                                                             flags | nat.MGN_BWD_DATA_ONLY, st))
-                    ev = torch.cuda.Event()
-                    ev.record(main)
-                    side.wait_event(ev)
-                    sp = nat._vp(side.cuda_stream)
-                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(w), w.numel(), kp, kb,
-                                                             ctypes.pointer(reds[2 * b]),
-                                                             flags | nat.MGN_BWD_WGRAD_ONLY, sp))
-                    if side_reduced:
-                        nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2, sp))
-                        if GRAD_READY is not None:  # final on the side stream: the bucket waits there
-                            with torch.cuda.stream(side):
-                                ready(G, blo, bhi)
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    done[b % nws] = ev
-                elif defer:
-                    nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(),
-                                                             ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
-                                                             ctypes.pointer(reds[2 * b]), flags, st))
-                    if GRAD_READY is not None:
-                        if pend_hi is None:
-                            pend_b, pend_hi = b, bhi
-                        if (pend_hi - blo) * 4 >= GRAD_GROUP_BYTES or b == 0:
-                            # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
-                            nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1),
-                                                              st))
-                            ready(G, blo, pend_hi)
-                            pend_hi = pend_b = None
-                elif not overlap:
-                    if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
-                        red2 = (nat.WgradReduce * 2)()
-                        nat.check(L.mgn_block_backward_deferred2(*args, nat.ptr(ws), ws.numel(), None, 0, red2,
-                                                                 flags, st))
-                    else:
-                        nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
-                    ready(G, blo, bhi)
+                sp = nat._vp(side.cuda_stream)
+                nat.check(L.mgn_block_backward_deferred3(*args, nat.ptr(w), w.numel(), kp, kb,
+                                                         ctypes.pointer(reds[2 * b]),
+                                                         flags | nat.MGN_BWD_WGRAD_ONLY, ctypes.byref(optsc), sp))
+                if side_reduced:
+                    nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2, sp))
+                    if GRAD_READY is not None:  # final on the side stream: the bucket waits there
+                        with torch.cuda.stream(side):
+                            ready(G, blo, bhi)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                done[b % nws] = ev
+            elif defer:
+                nat.check(L.mgn_block_backward_deferred3(*args, nat.ptr(ws), ws.numel(),
+                                                         ctypes.c_void_p(keep.data_ptr() + b * kb), kb,
+                                                         ctypes.pointer(reds[2 * b]), flags, ctypes.byref(opts0), st))
+                if GRAD_READY is not None:
+                    if pend_hi is None:
+                        pend_b, pend_hi = b, bhi
+                    if (pend_hi - blo) * 4 >= GRAD_GROUP_BYTES or b == 0:
+                        # blocks b..pend_b: consecutive descriptors from reds[2b] (a pointer INTO reds)
+                        nat.check(L.mgn_wgrad_reduce_many(ctypes.pointer(reds[2 * b]), 2 * (pend_b - b + 1),
+                                                          st))
+                        ready(G, blo, pend_hi)
+                        pend_hi = pend_b = None
+            elif not overlap:
+                if flags:  # reduced at once (keep = NULL), with the pair-layout hand-offs
+                    red2 = (nat.WgradReduce * 2)()
+                    nat.check(L.mgn_block_backward_deferred3(*args, nat.ptr(ws), ws.numel(), None, 0, red2,
+                                                             flags, ctypes.byref(opts0), st))
                 else:
-                    w = wss[b % 2]
-                    if done[b % 2] is not None:
-                        main.wait_event(done[b % 2])  # the side stream is done reading this workspace
-                    nat.check(L.mgn_block_backward_data(*args, nat.ptr(w), w.numel(), st))
-                    evd = torch.cuda.Event()
-                    evd.record(main)
-                    side.wait_event(evd)
-                    nat.check(L.mgn_block_backward_wgrad(*args, nat.ptr(w), w.numel(), nat._vp(side.cuda_stream)))
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    done[b % 2] = ev
-                    with torch.cuda.stream(side):
-                        ready(G, blo, bhi)
-                dx, de = dx1, de1
-            if conc and ENC_DATA_CAP:
-                # the encoders' backward runs beside block 0's ring launch: its weight-gradient launches take
-                # the data share of the chip too (capped at the ring's share they took 63 instead of ~40 us)
-                nat.check(L.mgn_set_grid_cus(caps[0], caps[0]))
+                    nat.check(L.mgn_block_backward(*args, nat.ptr(ws), ws.numel(), st))
+                ready(G, blo, bhi)
+            else:
+                w = wss[b % 2]
+                if done[b % 2] is not None:
+                    main.wait_event(done[b % 2])  # the side stream is done reading this workspace
+                nat.check(L.mgn_block_backward_data(*args, nat.ptr(w), w.numel(), st))
+                evd = torch.cuda.Event()
+                evd.record(main)
+                side.wait_event(evd)
+                nat.check(L.mgn_block_backward_wgrad(*args, nat.ptr(w), w.numel(), nat._vp(side.cuda_stream)))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                done[b % 2] = ev
+                with torch.cuda.stream(side):
+                    ready(G, blo, bhi)
+            dx, de = dx1, de1
+        # the encoders' backward runs beside block 0's ring launch: with ENC_DATA_CAP its weight-gradient
+        # launches take the data share of the chip too (optse; capped at the ring's share they took 63
+        # instead of ~40 us)
 
-            def join():  # the side stream's weight gradients are complete before their reduction
-                if conc:
-                    nat.check(L.mgn_set_grid_cus(0, 0))
-                    for ev in done:
-                        if ev is not None:
-                            main.wait_event(ev)
-
-            if defer and not defer_dense and (GRAD_READY is None or conc):
-                join()
-                if not side_reduced:
-                    nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
-            if overlap:
+        def join():  # the side stream's weight gradients are complete before their reduction
+            if conc:
                 for ev in done:
                     if ev is not None:
-                        main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
-            gx = gea = None
-            nx, nea = ctx.needs_input_grad[4], ctx.needs_input_grad[5]
-            if ctx.only_processor:
-                h = plan.specs[0].hidden
-                if nx:
-                    gx = dx[:, :h].float().contiguous()
-                if nea:
-                    gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous()
+                        main.wait_event(ev)
+
+        if defer and not defer_dense and (GRAD_READY is None or conc):
+            join()
+            if not side_reduced:
+                nat.check(L.mgn_wgrad_reduce_many(reds, 2 * nb, st))
+        if overlap:
+            for ev in done:
+                if ev is not None:
+                    main.wait_event(ev)  # gradients complete (and both workspaces free) on the main stream
+        gx = gea = None
+        nx, nea = ctx.needs_input_grad[4], ctx.needs_input_grad[5]
+        if ctx.only_processor:
+            h = plan.specs[0].hidden
+            if nx:
+                gx = dx[:, :h].float().contiguous()
+            if nea:
+                gea = _permute(de, topo.csc_eid, E, H, mdt, torch.float32, True, st)[:, :h].contiguous()
+        else:
+            ne, ee = plan.specs[0], plan.specs[1]
+            gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
+            gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
+            if defer_dense:
+                _mlp_bwd_deferred(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc,
+                                  nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[0]), ws, keeps[1],
+                                  ctypes.pointer(dreds[1]), st, optse)
+                _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                                  nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
+                                  ctypes.pointer(dreds[2]), st, optse)
+                join()
+                # ONE reduction for the whole model: decoder (unless reduced already), every processor
+                # block (unless reduced on the side stream), encoders
+                parts = ([] if early_dec else [dreds[0]]) + \
+                    ([reds[i] for i in range(2 * nb)] if defer and not side_reduced else []) + [dreds[1], dreds[2]]
+                allr = (nat.WgradReduce * len(parts))(*parts)
+                nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
             else:
-                ne, ee = plan.specs[0], plan.specs[1]
-                gxc = torch.empty((N, ne.in_dim), dtype=torch.float32, device=dev) if nx else None
-                gec = torch.empty((E, ee.in_dim), dtype=torch.float32, device=dev) if nea else None
-                if defer_dense:
-                    _mlp_bwd_deferred(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc,
-                                      nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[0]), ws, keeps[1],
-                                      ctypes.pointer(dreds[1]), st)
-                    _mlp_bwd_deferred(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
-                                      nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, keeps[2],
-                                      ctypes.pointer(dreds[2]), st)
-                    join()
-                    # ONE reduction for the whole model: decoder (unless reduced already), every processor
-                    # block (unless reduced on the side stream), encoders
-                    parts = ([] if early_dec else [dreds[0]]) + \
-                        ([reds[i] for i in range(2 * nb)] if defer and not side_reduced else []) + [dreds[1], dreds[2]]
-                    allr = (nat.WgradReduce * len(parts))(*parts)
-                    nat.check(L.mgn_wgrad_reduce_many(allr, len(allr), st))
-                else:
-                    _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
-                             ctypes.c_void_p(gp + 4 * off[0]), ws, st)
-                    _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
-                             nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
-                gx = gxc
-                if nea:
-                    gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
-                ready(G, off[0], off[1] + plan.specs[1].numel)
-        finally:
-            if conc:
-                L.mgn_set_grid_cus(0, 0)
+                _mlp_bwd(descs[0], xin, nat.MGN_F32, ne.in_dim, None, N, sv_ne[0], dx, mdt, gxc, nat.MGN_F32,
+                         ctypes.c_void_p(gp + 4 * off[0]), ws, st)
+                _mlp_bwd(descs[1], ein, nat.MGN_F32, ee.in_dim, topo.csc_eid, E, sv_ee[0], de, mdt, gec,
+                         nat.MGN_F32, ctypes.c_void_p(gp + 4 * off[1]), ws, st)
+            gx = gxc
+            if nea:
+                gea = _permute(gec, topo.csc_eid, E, ee.in_dim, nat.MGN_F32, torch.float32, True, st)
+            ready(G, off[0], off[1] + plan.specs[1].numel)
         if plan.padded:
             G = plan.unpad(G)
             _grad_ready(G, 0, plan.numel)
-        ctx.state = None
+        ctx.state = ctx.fwss = None
         return (None, None, None, None, gx, gea, None, *plan.grad_views(G))
 
 

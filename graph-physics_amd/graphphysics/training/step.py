@@ -63,10 +63,14 @@ def control_group(group=None):
     if dist.get_backend(group) == "gloo":
         return group if group is not None else dist.group.WORLD
     ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else None
-    g = _CTL_GROUPS.get(ranks)
-    if g is None:
-        g = _CTL_GROUPS[ranks] = dist.new_group(ranks=list(ranks) if ranks is not None else None, backend="gloo")
-    return g
+    # cached per rank set AND per default process group: after destroy_process_group() and a
+    # re-init (elastic restart, tests) the cached group belongs to a destroyed world and is rebuilt
+    world = dist.group.WORLD
+    ent = _CTL_GROUPS.get(ranks)
+    if ent is None or ent[0] is not world:
+        ent = _CTL_GROUPS[ranks] = (world, dist.new_group(ranks=list(ranks) if ranks is not None else None,
+                                                          backend="gloo"))
+    return ent[1]
 
 
 class TrainStep:

@@ -24,8 +24,8 @@
  * Conventions
  *  - All device memory is owned by the caller (PyTorch caching allocator); raw pointers + sizes.
  *    The library holds no device allocations and no global mutable state besides the
- *    thread-local error string. Every call is asynchronous on the given stream except
- *    mgn_topology_build (which reads back one validation word; mgn_topology_build_async does not).
+ *    thread-local error string (per-call options such as CU caps are arguments: mgn_call_opts;
+ *    ABI v17). Every call is asynchronous on the given stream except mgn_topology_build (which reads back one validation word; mgn_topology_build_async does not).
  *  - Input validation that needs the data (edge_index range, node-type range) never reads back to
  *    the host on the asynchronous entry points: kernels OR an MGN_ERR_* bit into a caller-owned
  *    device word (uint32, zeroed by the caller), keep every access in bounds (clamped index /
@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mgn_stream_t; /* == hipStream_t */
 
-#define MGN_ABI_VERSION 16
+#define MGN_ABI_VERSION 17
 #define MGN_F32 0
 #define MGN_BF16 1
 #define MGN_MAX_LAYERS 8
@@ -64,6 +64,9 @@ const char* mgn_last_error(void);
 #define MGN_ERR_EDGE_INDEX 1u /* edge_index outside [0, N): reference IndexError (ATen index)         */
 #define MGN_ERR_TYPE_NEG 2u   /* node type < 0 or NaN: F.one_hot "Class values must be non-negative." */
 #define MGN_ERR_TYPE_BIG 4u   /* node type >= n_types: "Class values must be smaller than num_classes." */
+#define MGN_ERR_HANDOFF 8u    /* ABI v17: a bounded hand-off wait inside a pipelined kernel (the recomputed
+                                 weight gradients, mgn_block_backward_deferred3) timed out; the kernel
+                                 wrote NaN into its partial sums instead of a partial result           */
 #define MGN_ERR_ANY 0xFFFFu   /* any validation error (bits 0-15)                                      */
 /* State updates are predicated on the word, so an error raised lazily (one call late) leaves the
  * training state as the reference's immediate exception would (ABI v11): mgn_adamw_dev skips its
@@ -267,7 +270,8 @@ int mgn_block_backward_deferred(const mgn_topology* t, const mgn_mlp* edge, cons
  * the data gradients (dx, de, and what the weight gradients read: dZ saves in `ws`, partials in
  * `keep`); WGRAD_ONLY then runs the block's single weight-gradient launch and fills reduce2. The
  * WGRAD_ONLY call may be issued on another stream (ordered after DATA_ONLY by the caller) and run
- * beside the next block's DATA_ONLY call on ANOTHER workspace; mgn_set_grid_cus gives each its CUs. */
+ * beside the next block's DATA_ONLY call on ANOTHER workspace; mgn_block_backward_deferred3's
+ * mgn_call_opts gives each its CUs. */
 #define MGN_BWD_DATA_ONLY 16
 #define MGN_BWD_WGRAD_ONLY 32
 int mgn_block_backward_deferred2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
@@ -288,12 +292,35 @@ int mgn_mlp_backward_deferred2(const mgn_mlp* m, const void* in, int32_t in_dtyp
                                const void* dout, int32_t dout_dtype, void* din, int32_t din_dtype,
                                float* grads, void* ws, size_t ws_bytes, void* keep, size_t keep_bytes,
                                mgn_wgrad_reduce* reduce1, int32_t flags, mgn_stream_t stream);
-/* ABI v13: caps on the CUs the persistent grids of later launches are sized for (0 = the whole
- * device): data_cus for every launch except the weight-gradient launches, wgrad_cus for those. Host
- * state of the library, read when a launch is issued (a captured hipGraph keeps the grids it
- * recorded); the results do not depend on the caps except for the weight-gradient slab partition
- * (summation order of the fp32 reductions). */
-int mgn_set_grid_cus(int32_t data_cus, int32_t wgrad_cus);
+/* ABI v17: per-call options of the backward entry points (NULL = none; replaces v13's process-global
+ * mgn_set_grid_cus, which two models or streams in one process shared):
+ *   data_cus / wgrad_cus  caps on the CUs the persistent grids of this call's launches are sized for
+ *                         (0 = the whole device): data_cus for every launch except the weight-gradient
+ *                         launches, wgrad_cus for those. The results do not depend on the caps except
+ *                         for the weight-gradient slab partition (summation order of the fp32 reductions).
+ *                         A captured hipGraph keeps the grids it recorded.
+ *   err_word              device word (as mgn_topology_build_async's) the call's pipelined kernels OR
+ *                         MGN_ERR_HANDOFF into when a bounded hand-off wait times out (NULL: the NaN
+ *                         partials alone report it). mgn_adamw_dev skips its update while it is set. */
+typedef struct mgn_call_opts {
+    int32_t data_cus;
+    int32_t wgrad_cus;
+    uint32_t* err_word;
+} mgn_call_opts;
+/* mgn_block_backward_deferred2 / mgn_mlp_backward_deferred2 with per-call options (same flags; for the
+ * MLP, flags 0 = the whole deferred call, mgn_mlp_backward_deferred). */
+int mgn_block_backward_deferred3(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node,
+                                 const void* x, const void* e, const mgn_block_saved* saved,
+                                 const void* dx_out, const void* de_out, void* dx, void* de,
+                                 float* edge_grads, float* node_grads, void* ws, size_t ws_bytes,
+                                 void* keep, size_t keep_bytes, mgn_wgrad_reduce* reduce2,
+                                 int32_t flags, const mgn_call_opts* opts, mgn_stream_t stream);
+int mgn_mlp_backward_deferred3(const mgn_mlp* m, const void* in, int32_t in_dtype, int64_t in_ld,
+                               const int32_t* in_rows, int64_t rows, const mgn_mlp_saved* saved,
+                               const void* dout, int32_t dout_dtype, void* din, int32_t din_dtype,
+                               float* grads, void* ws, size_t ws_bytes, void* keep, size_t keep_bytes,
+                               mgn_wgrad_reduce* reduce1, int32_t flags, const mgn_call_opts* opts,
+                               mgn_stream_t stream);
 /* Diagnostics builds (MGN_STAMPS) only, else an error status: per-wave [start, end] s_memrealtime ticks
  * (100 MHz) of the last launch of a chained kernel kind (0 edge fwd, 1 edge bwd, 2 node fwd, 3 node
  * bwd), n <= 4096 waves in workgroup-major order. */

@@ -55,6 +55,7 @@ class MaskRecorder:
         from graphphysics import _native as nat
 
         assert st["mdt"] == nat.MGN_F32, "mask pinning reads fp32 saves (bf16 rounds activations to 0)"
+        assert not st.get("rew"), "the recomputed weight gradients save no edge-MLP layer inputs to read masks from"
         torch.cuda.synchronize()
         plan, topo = st["plan"], st["topo"]
         N, E = topo.num_nodes, topo.num_edges

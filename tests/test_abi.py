@@ -61,6 +61,8 @@ int main(void) {
   P(mgn_mlp, norm_dim) P(mgn_pack_job, n_src) P(mgn_pack_job, kb_pad) P(mgn_block_saved, proj)
   printf("mgn_wgrad_reduce %zu\n", sizeof(mgn_wgrad_reduce));
   P(mgn_wgrad_reduce, nchunks_x) P(mgn_wgrad_reduce, hoff) P(mgn_wgrad_reduce, nchunks_h)
+  printf("mgn_call_opts %zu\n", sizeof(mgn_call_opts));
+  P(mgn_call_opts, wgrad_cus) P(mgn_call_opts, err_word)
   return 0;
 }
 """
@@ -91,12 +93,15 @@ int main(void) {
     assert int(got["mgn_wgrad_reduce"]) == ctypes.sizeof(nat.WgradReduce)
     for f in ("nchunks_x", "hoff", "nchunks_h"):
         assert int(got["mgn_wgrad_reduce." + f]) == getattr(nat.WgradReduce, f).offset
+    assert int(got["mgn_call_opts"]) == ctypes.sizeof(nat.CallOpts)
+    for f in ("wgrad_cus", "err_word"):
+        assert int(got["mgn_call_opts." + f]) == getattr(nat.CallOpts, f).offset
 
 
 def test_host_size_functions(lib):
     from graphphysics import _native as nat
 
-    assert lib.mgn_abi_version() == 16
+    assert lib.mgn_abi_version() == 17
     # fragment-packed Linear: max(fwd, transposed) fragment count x 64 lanes x VEC
     assert lib.mgn_linear_pack_elems(128, 384, nat.MGN_BF16) == max(8 * 12, 24 * 4) * 64 * 8
     assert lib.mgn_linear_pack_elems(2, 128, nat.MGN_F32) == max(1 * 32, 8 * 1) * 64
@@ -124,3 +129,26 @@ def test_errors_without_device_are_reported_not_crashing(lib):
     rc = lib.mgn_mlp_forward(ctypes.byref(m), None, 0, 8, None, 10, None, 0, ctypes.byref(s), None)
     assert rc != 0
     assert b"at least 2 layers" in lib.mgn_last_error()
+
+
+def test_no_process_global_launch_state(lib):
+    """ABI v17: the CU caps are per-call arguments (mgn_call_opts), so the header
+    declares no setter of library-wide state and says so; a negative cap is rejected by the call itself
+    (before any device work)."""
+    from graphphysics import _native as nat
+
+    decl = header_functions()
+    assert "mgn_set_grid_cus" not in decl and not any(n.startswith("mgn_set_") for n in decl)
+    src = open(HEADER).read()
+    assert "no global mutable state besides the" in src and "mgn_call_opts" in src
+    m = nat.Mlp()
+    m.n_layers, m.in_dim, m.hidden, m.out_dim, m.has_norm, m.dtype = 4, 8, 128, 128, 1, nat.MGN_BF16
+    bad = nat.CallOpts(-1, 0, None)
+    rc = lib.mgn_mlp_backward_deferred3(ctypes.byref(m), None, 0, 8, None, 10, None, None, 0, None, 0, None, None,
+                                        0, None, 0, ctypes.byref(nat.WgradReduce()), 0, ctypes.byref(bad), None)
+    assert rc != 0 and b"CU caps" in lib.mgn_last_error()
+    t = nat.Topology()
+    rc = lib.mgn_block_backward_deferred3(ctypes.byref(t), ctypes.byref(m), ctypes.byref(m), None, None, None, None,
+                                          None, None, None, None, None, None, 0, None, 0,
+                                          (nat.WgradReduce * 2)(), 0, ctypes.byref(nat.CallOpts(0, -4, None)), None)
+    assert rc != 0 and b"CU caps" in lib.mgn_last_error()

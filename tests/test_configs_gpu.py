@@ -354,7 +354,14 @@ def test_aneurysm_full_size_fp32_and_bf16_gradients(khop, mp, h):
     training_config/coarse-aneurysm.json); inputs node_in 23, edge_in 4, out 3.
       fp32: output rel-L2 <= 1e-4 vs the fp32 evaluation; output (1e-5), every parameter gradient and
             the input gradients (x, edge_attr) within SURVEY §8c's 1e-3 of the fp64 evaluation on
-            libmgn's ReLU branch (mask-pinned), every flipped unit a near-tie.
+            libmgn's ReLU branch (mask-pinned), every flipped unit a near-tie; AND, unpinned (VERDICT
+            r05 item 2: so libmgn's fp32 cannot drift from the reference's own fp32 distance to fp64),
+            every gradient within max(1.5e-3, 2 x the worst error the reference algorithm's fp32 shows
+            vs the unpinned fp64 evaluation over PyTorch's own order and 4 permuted summation orders
+            (tests/_orders.py order_spread)). The 1.5e-3 floor: near-ties flipped by any fp32 order move
+            upstream gradients by up to ~1e-3 (measured round 5: libmgn 1.06e-3 on block 12's edge W0,
+            PyTorch's fp32 2.5e-4 / 3.8e-4 in two runs), 4 orders need not sample the same tie, and
+            4 x 1.4M-edge fp32 orders is what the test budget holds (the Cfg B checks run 24).
       bf16: output and every gradient no further from fp64 than 2 x the bf16 autocast evaluation's
             error (floor 1e-2), and the SAME on the rows of the highest in-degree nodes alone (nodes with
             in-degree >= the 99th percentile): an indexing error confined to long segments would stand out
@@ -383,12 +390,25 @@ def test_aneurysm_full_size_fp32_and_bf16_gradients(khop, mp, h):
     p64 = _pinned_eval(ref, xin, ei, ea, gy, mp, rec.masks, stats)
     del rec
     assert _rel(g32["y"], p64["y"]) <= 1e-5, _rel(g32["y"], p64["y"])
-    worst = []
+    # the reference algorithm's fp32 spread vs the unpinned fp64 evaluation, in 4 more summation orders
+    gy32 = gy.to(DEV)
+    rp = {k: v.detach().to(DEV, torch.float32) for k, v in ref.named_parameters()}
+    sp = order_spread(lambda q, i: (_epd_ckpt(i["x"], ei, i["ea"], q, mp) * gy32).sum(), rp,
+                      {k: r64[k] for k in rp}, n_orders=4, seed=5,
+                      inputs={"x": (xin.to(DEV), "nodes_encoder.0.weight"),
+                              "ea": (ea.to(DEV).float(), "edges_encoder.0.weight")})
+    del rp
+    torch.cuda.empty_cache()
+    worst, worst_u = [], []
     for k in p64:
         e_got, e_unpinned, e_ref = _rel(g32[k], p64[k]), _rel(g32[k], r64[k]), _rel(r32[k], r64[k])
         worst.append((e_got, k, e_unpinned, e_ref))
         assert e_got <= 1e-3, (k, e_got, e_unpinned, e_ref)
+        bound = max(1.5e-3, 2 * max(e_ref, sp.get(k, 0.0)))
+        worst_u.append((e_unpinned / bound, k, e_unpinned, e_ref, sp.get(k)))
+        assert e_unpinned <= bound, ("unpinned", k, e_unpinned, e_ref, sp.get(k))
     print("\nfp32 worst pinned (libmgn vs pinned fp64, key, vs unpinned fp64, aten-fp32 vs fp64):", sorted(worst)[-3:])
+    print("fp32 worst unpinned (ratio to bound, key, libmgn, aten-fp32, worst permuted order):", sorted(worst_u)[-3:])
     print("fp32 branch flips:", dict(stats))
     for k, v in stats.items():
         assert v["max_rel_z"] <= 1e-4, f"{k}: libmgn's branch differs from fp64 away from a tie: {v}"

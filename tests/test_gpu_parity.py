@@ -1157,7 +1157,7 @@ def test_deferred_weight_gradient_reduction_is_bitwise_identical():
                                               (torch.float32, "0,0", 2)])
 def test_concurrent_weight_gradients_match_one_stream(dtype, caps, batch):
     """The processor backward with each block's weight-gradient launch on a side stream beside the
-    next block's data gradients (MGN_BWD_DATA_ONLY / _WGRAD_ONLY, mgn_set_grid_cus caps) computes the
+    next block's data gradients (MGN_BWD_DATA_ONLY / _WGRAD_ONLY, per-call mgn_call_opts caps) computes the
     same backward as one stream: input gradients bit-identical (every data-gradient kernel works per
     tile, whatever its grid); parameter gradients bit-identical when the weight-gradient launch keeps
     the whole chip (caps 0,0: same slab partition), else equal up to the fp32 summation order of the

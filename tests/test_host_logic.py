@@ -307,3 +307,34 @@ def test_concurrent_backward_regimes(monkeypatch):
     assert eng.conc_caps(88560, True) is None
     monkeypatch.setattr(eng, "CONC_WGRAD", "168,88")
     assert eng.conc_caps(11070, False) == (168, 88)
+
+
+def test_control_group_rebuilt_after_process_group_reinit(monkeypatch):
+    """TrainStep's host-side control group (training/step.py control_group) is cached per rank
+    set AND per default process group: after destroy_process_group() and a re-init in the same process the
+    next TrainStep gets a live group, not the destroyed world's. A 1-rank gloo world posing as an RCCL one
+    (get_backend patched), so the cached-gloo-group path runs on the CPU."""
+    import socket
+
+    import torch.distributed as dist
+    from graphphysics.training import step as S
+
+    def port():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            return s.getsockname()[1]
+
+    monkeypatch.setattr(S.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(S, "_CTL_GROUPS", {})
+    got = []
+    for _ in range(2):
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port(), rank=0, world_size=1)
+        try:
+            g = S.control_group()
+            assert S.control_group() is g  # cached within one world
+            t = torch.ones(1)
+            dist.all_reduce(t, group=g)  # usable
+            got.append(g)
+        finally:
+            dist.destroy_process_group()
+    assert got[0] is not got[1]

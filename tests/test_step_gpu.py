@@ -219,6 +219,42 @@ def test_bad_edge_index_skips_the_optimizer_update(graph):
     assert float(after["node_norm"]["_acc_count"] - before["node_norm"]["_acc_count"]) == float(good.x.shape[0])
 
 
+def test_recompute_handoff_timeout_raises_and_skips_the_update(monkeypatch):
+    """VERDICT r05 item 3 / ADVICE r05: a hand-off wait of the recomputed edge weight gradients
+    (chain16_rew_kernel) that gives up must never become a silently wrong gradient. Forced here with
+    MGN_REW_SPIN=0 (every wait gives up at once) on the recompute path (MGN_REW=1): the kernel ORs
+    MGN_ERR_HANDOFF into the error word passed with the call (mgn_call_opts, ABI v17) and writes NaN
+    partial sums; AdamW skips its update on the word (parameters and moments untouched), the next step
+    raises RuntimeError and rewinds the host counters; with the waits restored training continues."""
+    from graphphysics.models import _engine
+
+    monkeypatch.setattr(_engine, "REW", "1")
+    sim, opt, sch, st = _train(False)
+    st()
+    torch.cuda.synchronize()
+    before = _state(sim, opt, sch)
+    monkeypatch.setenv("MGN_REW_SPIN", "0")
+    st()  # the backward's recompute launches time out; this step's AdamW sees the word and skips
+    torch.cuda.synchronize()
+    grads = [p.grad for p in sim.parameters() if p.grad is not None]
+    assert any(bool(torch.isnan(g).any()) for g in grads), "timed-out partial sums must poison the gradients"
+    monkeypatch.delenv("MGN_REW_SPIN")
+    with pytest.raises(RuntimeError, match="hand-off"):
+        for _ in range(2):
+            st()
+            torch.cuda.synchronize()
+    after = _state(sim, opt, sch)
+    for k in ("params", "moments"):
+        assert _same(after[k], before[k]), k
+    assert (after["step_count"], after["lr"], after["last_epoch"]) == \
+        (before["step_count"], before["lr"], before["last_epoch"])
+    loss = st()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all()
+    assert all(torch.isfinite(p.grad).all() for p in sim.parameters() if p.grad is not None)
+    assert opt.param_groups[0]["step_count"] == before["step_count"] + 1
+
+
 def test_data_parallel_graph_bad_edge_index_raises_index_error():
     """a data-parallel captured step whose re-capture warm-up meets a bad edge_index must
     undo the warm-up (its divergence mark included), run the batch once eagerly and raise the
