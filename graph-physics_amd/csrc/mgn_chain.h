@@ -21,6 +21,13 @@ struct ChainFwdArgs {
     int64_t act_off[4];
     unsigned* mask32;           // [3][ntiles*64] 32-bit lane words (ReLU bits)
     int64_t mask_stride;        // 64-bit words per layer
+    // round 6, edge-side aggregation (EdgeAgg: graphs of high in-degree): the tile's segment sums of the
+    // messages s ⊙ z / q over its runs of equal dst (fp32 [*][128] rows): complete segments into
+    // agg_full[dst], a run continuing from the previous tile into agg_head[tile], one continuing into
+    // the next tile into agg_tail[tile]
+    float* agg_full;
+    float* agg_head;
+    float* agg_tail;
 };
 
 // Edge MLP weight gradients of layers 1..3 with their inputs RECOMPUTED (round 5): the forward writes no
@@ -94,6 +101,11 @@ struct ChainNodeFwdArgs {
     const float* pn_b0;         // its layer-0 bias (folded into P_i)
     __bf16* pn_out;             // [N][256] bf16: P_i ‖ P_j
     int32_t pn_kst;             // k-steps per row tile of its layer-0 pack
+    // edge-side aggregation (round 6; the edge forward's ChainFwdArgs agg_*): aggr[v] = agg_full[v] when
+    // v's in-edges lie in one 16-edge tile, else agg_tail[tb] + agg_head[tb + 1] + ... + agg_head[te]
+    const float* agg_full;
+    const float* agg_head;
+    const float* agg_tail;
 };
 
 struct ChainNodeBwdArgs {
@@ -121,9 +133,14 @@ int chain16_node_backward_parts(int64_t M);
 bool chain_node_eligible(const mgn_mlp* m);  // bf16, 256 -> 128 -> 128, 4 layers, RMSNorm
 // next_edge / next_proj (optional): also write the next block's node projections (bf16 [N][2·128],
 // b0 folded into P_i) from x_out — the chained edge forward's proj input, without its own launch
+// agg_scratch (optional, chain16_edge_agg_bytes): the edge forward already summed the messages per tile
+// run (EdgeAgg) — the node forward adds those partial rows instead of gathering every in-edge's z
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
-                         hipStream_t st, const mgn_mlp* next_edge = nullptr, void* next_proj = nullptr);
+                         hipStream_t st, const mgn_mlp* next_edge = nullptr, void* next_proj = nullptr,
+                         void* agg_scratch = nullptr);
+// EdgeAgg scratch: [N][128] + 2 x [rows_pad(E)/16][128] fp32 (full / head / tail partial rows)
+size_t chain16_edge_agg_bytes(int64_t N, int64_t E);
 // din2: dout (dx_out) in the pair layout (mgn_block_backward_deferred2, MGN_BWD_DX_OUT_PAIR)
 int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, void* dz8,
                           float* dscale_part, int* nparts, void* dx_part, void* d_aggr, hipStream_t st,
@@ -135,7 +152,8 @@ int chain16_node_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
 // save_act = false (the recomputed weight gradients, chain16_edge_wgrad_recompute): ReLU masks, z and rden
 // only — no R8 layer inputs
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act = true);
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act = true,
+                         int64_t N = 0, void* agg_scratch = nullptr);
 // dW / db of the edge MLP's layers 1..3 into slabs part[0 .. nchunks) (chunks of rows_per_chunk rows, a
 // multiple of 32), their inputs recomputed from e and the projections (ChainRewArgs)
 int chain16_edge_wgrad_recompute(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,

@@ -354,13 +354,81 @@ __device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, in
     dj = a.proj_j[row];
 }
 
+// EdgeAgg (round 6): the dst of the rows adjoining the tile — lane 0 gets row 16·tile − 1's, lane 15 row
+// 16·tile + 16's (-1 where there is none); the other lanes' values are unused
+__device__ __forceinline__ int load_nb(const ChainFwdArgs& a, int64_t tile, int lane) {
+    const int m = lane & 15;
+    const int64_t r = m == 0 ? tile * TR - 1 : tile * TR + TR;
+    const bool ok = r >= 0 && r < a.M && (m == 0 || m == 15);
+    const int v = a.proj_i[ok ? r : 0];
+    return ok ? v : -1;
+}
+
+// EdgeAgg: the messages v (this lane's row m, features 16t + 4g + r; 0 for rows >= M) summed over each
+// run of equal dst among the tile's 16 rows — a segmented inclusive scan over the 16 lanes of each DPP row
+// (row_shr 1, 2, 4, 8; a tile of one run, the common case at high in-degree, skips the segment tests)
+// — then the run's last lane stores its sum: a segment that starts and ends in this tile into
+// agg_full[dst], the run continuing from the previous tile into agg_head[tile], the one continuing
+// into the next tile into agg_tail[tile] (rows sorted by dst: at most one of each per tile). Fixed
+// order: deterministic; the node forward adds the partial rows of a segment in tile order.
+__device__ __forceinline__ int dpp_shr_i(int v, int d) {
+    switch (d) {
+        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+        case 4: return __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+        default: return __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    }
+}
+__device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64_t tile, int lane,
+                                               const ChainFwdArgs& a) {
+    const int m = lane & 15, g = lane >> 4;
+    const int dprev = __builtin_amdgcn_update_dpp(-1, di, 0x111, 0xF, 0xF, false);  // row_shr:1 (m = 0 keeps -1)
+    const int dnext = __builtin_amdgcn_update_dpp(-1, di, 0x101, 0xF, 0xF, false);  // row_shl:1 (m = 15 keeps -1)
+    const bool first = m == 0 || dprev != di;
+    const bool last = m == 15 || dnext != di;
+    const int nb0 = __shfl(nb, lane & 48);  // lane 0 of this DPP row: the previous tile's last dst
+    int rs = 0;                             // first lane of this lane's run
+    if (__builtin_amdgcn_ballot_w64(first) == 0x0001000100010001ull) {
+        // one run: plain prefix sums (lane 15 ends with the total)
+#pragma unroll
+        for (int d = 1; d <= 8; d *= 2)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    v[t][r] += __int_as_float(dpp_shr_i(__float_as_int(v[t][r]), d));
+    } else {
+        rs = first ? m : 0;
+#pragma unroll
+        for (int d = 1; d <= 8; d *= 2) rs = max(rs, dpp_shr_i(rs, d));
+#pragma unroll
+        for (int d = 1; d <= 8; d *= 2) {
+            const bool ok = m - d >= rs;
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float sh = __int_as_float(dpp_shr_i(__float_as_int(v[t][r]), d));
+                    v[t][r] += ok ? sh : 0.f;
+                }
+        }
+    }
+    if (!last || tile * TR >= a.M) return;
+    const bool sb = rs == 0 && nb0 == di;  // the run holds lane 0 and continues from the previous tile
+    const bool ca = m == 15 && nb == di;   // it continues into the next tile
+    float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(dst + 16 * t + 4 * g) = v[t];
+}
+
 // SAVE = false: inference (no autograd): only z and rden (the node MLP's aggregation inputs) are
 // written — no R8 layer inputs, no ReLU masks (≈ 40 % of the training forward's HBM bytes).
 // P is in the pair layout; ZP2: z too (the chained node MLP and the chained backward read it so;
 // false: row-major, for a generic node MLP)
 // SACT = false (with SAVE): ReLU masks, z, rden but no R8 layer inputs (their weight gradients recompute
 // them: chain16_rew_kernel)
-template <bool SAVE, int NWK, bool ZP2, bool SACT = true>
+// EAGG (round 6, with SAVE): also the edge-side aggregation of the messages (edge_agg_store)
+template <bool SAVE, int NWK, bool ZP2, bool SACT = true, bool EAGG = false>
 __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -374,8 +442,9 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     STAMP_DECL;
     WAVE_T0;
     In16 nxt;
-    int di, dj;
+    int di, dj, nb = -1;
     load_idx(a, min(tile, last), lane, di, dj);
+    if (EAGG) nb = load_nb(a, min(tile, last), lane);
     load_e(nxt, a, min(tile, last), lane);
     stage16<4, NWK * 64>(W, a.wpack, a.woff, a.wks, false);
     for (int i = threadIdx.x; i < 5 * H; i += NWK * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
@@ -385,6 +454,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
     pin(di);
     pin(dj);
+    if (EAGG) pin(nb);
     STAMP(0);
     for (; tile < a.ntiles; tile += stride) {
         const In16 in = nxt;
@@ -397,8 +467,9 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
             load_p2(pi, a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : di) * (2 * H), g);
             load_p2(pj, a.proj + (int64_t)((MGN_ABLATE & 1) ? 0 : dj) * (2 * H) + H, g);
         }
-        int ndi, ndj;
+        int ndi, ndj, nnb = -1;
         load_idx(a, min(tile + stride, last), lane, ndi, ndj);
+        if (EAGG) nnb = load_nb(a, min(tile + stride, last), lane);
         load_e(nxt, a, min(tile + stride, last), lane);
         const int64_t row = tile * TR + m;
         f4 acc[8];
@@ -447,6 +518,11 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         if (g == 0 && row < a.M) a.rden_save[row] = q;
         store_rows<ZP2>(acc, scr, a.z_save, tile, a.M, lane);
         STAMP(5);
+        bf16x4 zb[8];  // EAGG: the bf16 z the messages are made of (the node forward's terms)
+        if (EAGG) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) zb[t] = bf16x4{(__bf16)acc[t][0], (__bf16)acc[t][1], (__bf16)acc[t][2], (__bf16)acc[t][3]};
+        }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
@@ -455,6 +531,17 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
                 acc[t][r] = fmaf(s[r], acc[t][r] * rq, (float)in.eb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
+        if (EAGG) {
+            // the messages s ⊙ z / q as the node forward's aggregation takes them (bf16 z, 1/q, then s)
+            const bool live = row < a.M;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[t][r] = live ? s[r] * ((float)zb[t][r] * rq) : 0.f;
+            }
+            edge_agg_store(acc, di, nb, tile, lane, a);
+        }
         STAMP(6);
 #pragma unroll
         for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
@@ -462,6 +549,10 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         pin(ndj);
         di = ndi;
         dj = ndj;
+        if (EAGG) {
+            pin(nnb);
+            nb = nnb;
+        }
         STAMP(7);
     }
     STAMP_PRINT("fwd16");
@@ -775,7 +866,9 @@ __device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int
 }
 
 // SAVE = false: inference — no aggregate, R8, mask, z or rden saves
-template <bool SAVE>
+// EAGG (round 6): the aggregate from the edge forward's per-tile partial rows (edge_agg_store) instead of
+// every in-edge's z: agg_full[v], or agg_tail[tb] + agg_head[tb + 1] + ... + agg_head[te] in tile order
+template <bool SAVE, bool EAGG = false>
 __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -806,6 +899,34 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
             const u32x2 hi = *reinterpret_cast<const u32x2*>(xp + 32 * s + 16);
             const u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
             xb[s] = __builtin_bit_cast(bf16x8, w);
+        }
+        if (EAGG) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) agg[t] = f4{0.f, 0.f, 0.f, 0.f};
+            if (kb < ke) {
+                const int tb = kb >> 4, te = (ke - 1) >> 4;
+                const float* p0 = tb == te ? a.agg_full + v * H : a.agg_tail + (int64_t)tb * H;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) agg[t] = *reinterpret_cast<const f4*>(p0 + 16 * t + 4 * g);
+                // the head rows of the tiles after tb, two per round trip (the second clamped, added as 0)
+#pragma unroll 1
+                for (int T = tb + 1; T <= te; T += 2) {
+                    const int T2 = T + 1 <= te ? T + 1 : T;
+                    f4 h0[8], h1[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        h0[t] = *reinterpret_cast<const f4*>(a.agg_head + (int64_t)T * H + 16 * t + 4 * g);
+                        h1[t] = *reinterpret_cast<const f4*>(a.agg_head + (int64_t)T2 * H + 16 * t + 4 * g);
+                    }
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) agg[t] += h0[t];
+                    if (T + 1 <= te) {
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) agg[t] += h1[t];
+                    }
+                }
+            }
+            return;
         }
         float* scv = reinterpret_cast<float*>(scr);  // [H] edge scale, private to the wave
         scv[2 * lane] = a.agg_scale[2 * lane];
@@ -1531,10 +1652,28 @@ __global__ __launch_bounds__(NW * 64) void chain16_dense_bwd_kernel(ChainDenseBw
 
 }  // namespace
 
+// EdgeAgg scratch carve: full [N][128], head / tail [rows_pad(E)/16][128] (fp32, 256-byte aligned parts)
+static size_t agg_al(size_t x) { return (x + 255) & ~(size_t)255; }
+size_t chain16_edge_agg_bytes(int64_t N, int64_t E) {
+    const int64_t nt = rows_pad(E) / TR;
+    return agg_al((size_t)N * H * 4) + 2 * agg_al((size_t)nt * H * 4);
+}
+static void agg_carve(void* scratch, int64_t N, int64_t E, float** full, float** head, float** tail) {
+    char* p = reinterpret_cast<char*>(scratch);
+    *full = reinterpret_cast<float*>(p);
+    p += agg_al((size_t)N * H * 4);
+    *head = reinterpret_cast<float*>(p);
+    p += agg_al((size_t)(rows_pad(E) / TR) * H * 4);
+    *tail = reinterpret_cast<float*>(p);
+}
+
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
-                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act) {
+                         int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act, int64_t N,
+                         void* agg_scratch) {
     ChainFwdArgs a;
     memset(&a, 0, sizeof(a));
+    const bool eagg = agg_scratch != nullptr;
+    if (eagg) agg_carve(agg_scratch, N, M, &a.agg_full, &a.agg_head, &a.agg_tail);
     a.e = reinterpret_cast<const __bf16*>(e);
     a.proj = reinterpret_cast<const __bf16*>(proj);
     a.proj_i = pi;
@@ -1558,7 +1697,10 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
     // inference (no saves) always feeds the chained node MLP: z in the pair layout
     MGN_REQUIRE(sv->act || z_p2, "chained inference edge forward: z must be in the pair layout");
     MGN_REQUIRE(save_act || (sv->act && z_p2), "edge forward without R8 saves: the chained block path only");
-    const auto kern = nwk == 12 ? (!sv->act   ? chain16_fwd_kernel<false, 12, true>
+    MGN_REQUIRE(!eagg || (sv->act && z_p2 && nwk == 12), "edge-side aggregation: the chained training forward only");
+    const auto kern = eagg ? (save_act ? chain16_fwd_kernel<true, 12, true, true, true>
+                                       : chain16_fwd_kernel<true, 12, true, false, true>)
+                    : nwk == 12 ? (!sv->act   ? chain16_fwd_kernel<false, 12, true>
                                    : !save_act ? chain16_fwd_kernel<true, 12, true, false>
                                    : z_p2      ? chain16_fwd_kernel<true, 12, true>
                                                : chain16_fwd_kernel<true, 12, false>)
@@ -1643,9 +1785,16 @@ bool chain_node_eligible(const mgn_mlp* m) {
 
 int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t, const mgn_mlp* edge,
                          const mgn_mlp_saved* edge_sv, int64_t M, void* x_out, void* aggr_save, mgn_mlp_saved* sv,
-                         hipStream_t st, const mgn_mlp* next_edge, void* next_proj) {
+                         hipStream_t st, const mgn_mlp* next_edge, void* next_proj, void* agg_scratch) {
     ChainNodeFwdArgs a;
     memset(&a, 0, sizeof(a));
+    if (agg_scratch) {
+        float *full, *head, *tail;
+        agg_carve(agg_scratch, t->num_nodes, t->num_edges, &full, &head, &tail);
+        a.agg_full = full;
+        a.agg_head = head;
+        a.agg_tail = tail;
+    }
     if (next_edge && next_proj) {
         a.pn_pack = reinterpret_cast<const __bf16*>(next_edge->wpack);  // layer 0 is the first pack
         a.pn_b0 = next_edge->bias[0];
@@ -1673,7 +1822,9 @@ int chain16_node_forward(const mgn_mlp* m, const void* x, const mgn_topology* t,
     a.mask32 = reinterpret_cast<unsigned*>(sv->mask);
     a.mask_stride = mask_words_per_layer(*m, M);
     if (M == 0) return 0;
-    const auto kern = sv->act ? chain16_node_fwd_kernel<true> : chain16_node_fwd_kernel<false>;
+    MGN_REQUIRE(!agg_scratch || sv->act, "edge-side aggregation: the chained training forward only");
+    const auto kern = agg_scratch ? chain16_node_fwd_kernel<true, true>
+                                  : sv->act ? chain16_node_fwd_kernel<true> : chain16_node_fwd_kernel<false>;
     if (int e2 = set_lds_once((const void*)kern, LDS_TOTAL)) return e2;
     ProfScope ps(PROF_FWD_NODE, st);
     hipLaunchKernelGGL(kern, dim3(node_grid(a.ntiles)), dim3(NW * 64), LDS_TOTAL, st, a);

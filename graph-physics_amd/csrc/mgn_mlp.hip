@@ -4288,10 +4288,25 @@ size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* e
     return block_fwd_ws(t, edge);
 }
 
+// Edge-side aggregation (round 6, chain16_fwd_kernel EAGG): for graphs of high in-degree the edge
+// forward sums each 16-edge tile's messages per run of equal dst and the node forward adds those partial
+// rows (about deg/16 + 1 per node) instead of gathering every in-edge's z row — at Cfg E (in-degree 62)
+// the node forward's 0.36 GB of z gathers per block. MGN_EDGE_AGG: "auto" (default: E >= 16 N), "1"
+// (every chained training block), "0" (never). The partial sums re-associate the fp32 aggregation (fixed
+// order, deterministic); the per-edge messages are the same bf16-z terms.
+static bool edge_agg_mode(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    if (!(chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0)) return false;
+    const char* v = getenv("MGN_EDGE_AGG");
+    if (v && v[0] == '0') return false;
+    if (v && v[0] == '1') return true;
+    return t->num_edges >= 16 * t->num_nodes;
+}
+
 static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
                               const void* e, void* x_out, void* e_out, mgn_block_saved* saved, void* ws,
                               size_t ws_bytes, int proj_ready, const mgn_mlp* next_edge, void* next_ws,
-                              size_t next_ws_bytes, int* next_proj_ready, mgn_stream_t stream) {
+                              size_t next_ws_bytes, int* next_proj_ready, mgn_stream_t stream,
+                              void* scratch = nullptr, size_t scratch_bytes = 0) {
     if (next_proj_ready) *next_proj_ready = 0;
     if (int r = check_mlp(edge)) return r;
     if (int r = check_mlp(node)) return r;
@@ -4351,9 +4366,16 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
         ein.K0 = 3 * H;
         ein.proj = nullptr;
     }
+    // edge-side aggregation: a training forward given the scratch (mgn_block_forward_scratch_bytes)
+    void* agg = nullptr;
+    if (chain && !infer && scratch && edge_agg_mode(t, edge, node)) {
+        MGN_REQUIRE(scratch_bytes >= chain16_edge_agg_bytes(t->num_nodes, t->num_edges),
+                    "block forward scratch too small (mgn_block_forward_scratch_bytes)");
+        agg = scratch;
+    }
     if (chain) {
         if (int r = chain16_edge_forward(edge, e, proj, t->csc_dst, t->csc_src, t->num_edges, e_out, &saved->edge, st,
-                                         chain_node_eligible(node), !rew))
+                                         chain_node_eligible(node), !rew, t->num_nodes, agg))
             return r;
     } else if (int r = mlp_fwd_any(edge, MODE_EDGE, ein, t->num_edges, e_out, dt, H, e, &saved->edge, t, nullptr,
                                    nullptr, nullptr, st)) {
@@ -4363,7 +4385,7 @@ static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const 
         const bool fuse = next_edge && next_ws && chain_eligible(next_edge) && next_edge->hidden == H &&
                           next_ws_bytes >= block_fwd_ws(t, next_edge) && t->num_nodes > 0;
         if (int r = chain16_node_forward(node, x, t, edge, &saved->edge, t->num_nodes, x_out, saved->aggr,
-                                         &saved->node, st, fuse ? next_edge : nullptr, fuse ? next_ws : nullptr))
+                                         &saved->node, st, fuse ? next_edge : nullptr, fuse ? next_ws : nullptr, agg))
             return r;
         if (fuse && next_proj_ready) *next_proj_ready = 1;
         return 0;
@@ -4396,6 +4418,19 @@ int mgn_block_forward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp*
                       mgn_stream_t stream) {
     return block_forward_impl(t, edge, node, x, e, x_out, e_out, saved, ws, ws_bytes, 0, nullptr, nullptr, 0, nullptr,
                               stream);
+}
+
+size_t mgn_block_forward_scratch_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+    return edge_agg_mode(t, edge, node) ? chain16_edge_agg_bytes(t->num_nodes, t->num_edges) : 0;
+}
+
+int mgn_block_forward_chain2(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
+                             const void* e, void* x_out, void* e_out, mgn_block_saved* saved, void* ws,
+                             size_t ws_bytes, int proj_ready, const mgn_mlp* next_edge, void* next_ws,
+                             size_t next_ws_bytes, int* next_proj_ready, void* scratch, size_t scratch_bytes,
+                             mgn_stream_t stream) {
+    return block_forward_impl(t, edge, node, x, e, x_out, e_out, saved, ws, ws_bytes, proj_ready, next_edge, next_ws,
+                              next_ws_bytes, next_proj_ready, stream, scratch, scratch_bytes);
 }
 
 int mgn_block_forward_chain(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,

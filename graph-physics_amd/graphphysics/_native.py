@@ -101,6 +101,10 @@ EXPORTS = {
     "mgn_block_forward_chain": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
                                        _vp, _vp, _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _sz, _i32,
                                        ctypes.POINTER(Mlp), _vp, _sz, ctypes.POINTER(ctypes.c_int32), _vp]),
+    "mgn_block_forward_scratch_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp)]),
+    "mgn_block_forward_chain2": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),
+                                        _vp, _vp, _vp, _vp, ctypes.POINTER(BlockSaved), _vp, _sz, _i32,
+                                        ctypes.POINTER(Mlp), _vp, _sz, ctypes.POINTER(ctypes.c_int32), _vp, _sz, _vp]),
     "mgn_block_backward_workspace_bytes": (_sz, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp),
                                                  ctypes.POINTER(Mlp)]),
     "mgn_block_backward": (_i32, [ctypes.POINTER(Topology), ctypes.POINTER(Mlp), ctypes.POINTER(Mlp),

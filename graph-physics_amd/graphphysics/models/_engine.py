@@ -611,6 +611,14 @@ class EPDFunction(torch.autograd.Function):
             nat.lib().mgn_block_forward_inference_supported(ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]))
             for b in range(nb))
         fwss = [_fwd_ws_block(topo, bdescs[0], bdescs[1], dev) for _ in range(nb if rew else 2)] if nb else None
+        # edge-side aggregation scratch (ABI v17, mgn_block_forward_chain2: graphs of high in-degree), one
+        # buffer for every block of the stack (each block's partial rows are dead after its node forward)
+        agg_scratch = None
+        if train and nb:
+            sb = int(nat.lib().mgn_block_forward_scratch_bytes(ctypes.byref(topo.struct), ctypes.byref(bdescs[0]),
+                                                               ctypes.byref(bdescs[1])))
+            if sb:
+                agg_scratch = torch.empty(sb, dtype=torch.uint8, device=dev)
         ready = ctypes.c_int32(0)
         for b in range(nb):
             es_, ns_ = bspecs[2 * b], bspecs[2 * b + 1]
@@ -632,11 +640,11 @@ class EPDFunction(torch.autograd.Function):
                 sv[0].proj = fws.data_ptr()
             nxt = ctypes.byref(bdescs[2 * b + 2]) if CHAIN_PROJ and b + 1 < nb else None
             proj_ready = ready.value
-            nat.check(nat.lib().mgn_block_forward_chain(
+            nat.check(nat.lib().mgn_block_forward_chain2(
                 ctypes.byref(topo.struct), ctypes.byref(bdescs[2 * b]), ctypes.byref(bdescs[2 * b + 1]),
                 nat.ptr(xs[-1]), nat.ptr(es[-1]), nat.ptr(x1), nat.ptr(e1), ctypes.byref(sv[0]), nat.ptr(fws),
                 fws.numel(), proj_ready, nxt, nat.ptr(nws) if nxt is not None else None, nws.numel(),
-                ctypes.byref(ready), st))
+                ctypes.byref(ready), nat.ptr(agg_scratch), agg_scratch.numel() if agg_scratch is not None else 0, st))
             if train:
                 xs.append(x1)
                 es.append(e1)

@@ -1,0 +1,180 @@
+"""Edge-side aggregation (round 6; include/mgn.h mgn_block_forward_chain2, MGN_EDGE_AGG): for graphs of high
+in-degree the chained bf16 edge-MLP forward sums each 16-edge tile's messages s ⊙ z / q per run of equal
+target and the node-MLP forward adds those partial rows (agg_full / agg_tail + agg_head ...) instead of
+re-reading every in-edge's z (reference layers.py:694-696, the sum aggregation).
+
+* the aggregate the node MLP consumed (its bf16 save, read through the INSPECT hook) equals an fp64 sum of
+  the same per-edge terms (the edge forward's bf16 z, 1/q, the RMSNorm scale) over each node's in-edges,
+  to bf16 rounding — a partial row dropped, doubled or misfiled is an O(1) error on that node — on graphs
+  built for the run bookkeeping's corner cases (no in-edges, one, runs ending exactly at a tile boundary,
+  runs spanning many tiles, E not a multiple of 16) and on a low-degree mesh (many runs per tile: the
+  segmented-scan path);
+* the whole model (forward and every gradient) is no further from fp64 than 2 x PyTorch's bf16 autocast of
+  the reference, like every bf16 check (tests/test_gpu_parity.py);
+* auto mode picks it exactly for E >= 16 N.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mgn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+H = 128
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    import __graft_entry__ as ge
+
+    ge.build()
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+
+
+def relerr(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _unpair(zp, rows):
+    """[rows, 128] row-major from the pair layout (feature 16t + 4g + r at 32(t>>1) + 8g + 4(t&1) + r)."""
+    zp = zp[: rows * H].view(rows, H)
+    col = torch.empty(H, dtype=torch.long)
+    for t in range(8):
+        for g in range(4):
+            for r in range(4):
+                col[16 * t + 4 * g + r] = 32 * (t >> 1) + 8 * g + 4 * (t & 1) + r
+    return zp[:, col.to(zp.device)]
+
+
+def _corner_graph(seed=3):
+    """In-degrees chosen for the tile bookkeeping: 0, 1, 15, 16, 17, 31, 32, 33, 100, and a random bulk."""
+    g = torch.Generator().manual_seed(seed)
+    degs = [0, 1, 15, 16, 17, 0, 31, 32, 33, 100, 2, 0, 64, 5]
+    n = 200
+    degs = degs + torch.randint(0, 70, (n - len(degs),), generator=g).tolist()
+    dst = torch.cat([torch.full((d,), v, dtype=torch.long) for v, d in enumerate(degs)])
+    e = dst.numel()
+    src = torch.randint(0, n, (e,), generator=g)
+    perm = torch.randperm(e, generator=g)  # the library sorts by target itself
+    return n, torch.stack([src[perm], dst[perm]])
+
+
+def _random_graph(n, e, seed):
+    g = torch.Generator().manual_seed(seed)
+    return n, torch.randint(0, n, (2, e), generator=g)
+
+
+def _cylinder():
+    from graphphysics.utils import meshes
+
+    b = meshes.cylinder_batch(2, jitter=0.01)
+    return b["x"].shape[0], torch.from_numpy(b["edge_index"])
+
+
+def _run(n, ei, mode, monkeypatch, mp=3, seed=11, record=False):
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+    from graphphysics.utils.data import Data
+
+    monkeypatch.setenv("MGN_EDGE_AGG", mode)
+    g = torch.Generator().manual_seed(seed)
+    e = ei.shape[1]
+    x = torch.randn(n, 11, generator=g)
+    ea = torch.randn(e, 3, generator=g)
+    gy = torch.randn(n, 2, generator=g)
+    torch.manual_seed(0)
+    m = EncodeProcessDecode(mp, 11, 3, 2, H, compute_dtype=torch.bfloat16).to(DEV)
+    seen = {}
+
+    def hook(st):
+        torch.cuda.synchronize()
+        topo = st["topo"]
+        seen["col_ptr"] = topo.col_ptr.long().cpu()
+        seen["blocks"] = [(ke[2].clone(), ke[3].clone(), aggr.clone()) for _, (ke, kn, aggr) in st["svs"]]
+
+    _engine.INSPECT = hook if record else None
+    try:
+        xd = x.to(DEV).requires_grad_(True)
+        y = m(Data(x=xd, edge_index=ei.to(DEV), edge_attr=ea.to(DEV)))
+    finally:
+        _engine.INSPECT = None
+    (y * gy.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    scales = [dict(m.named_parameters())[f"processor_list.{b}.edge_block.7.scale"].detach().double().cpu()
+              for b in range(mp)]
+    return y.detach(), xd.grad.detach(), grads, seen, scales, (x, ea, gy)
+
+
+def _check_aggregates(seen, scales, n, e):
+    """Each block's saved aggregate vs the fp64 sum of its own per-edge terms."""
+    cp = seen["col_ptr"]
+    seg = torch.repeat_interleave(torch.arange(n), cp[1:] - cp[:-1])
+    worst = 0.0
+    for (zp, rden, aggr), s in zip(seen["blocks"], scales):
+        z = _unpair(zp, e).double().cpu()
+        q = rden[:e].double().cpu()
+        terms = s[None, :] * (z / q[:, None])
+        ref = torch.zeros(n, H, dtype=torch.float64).index_add_(0, seg, terms)
+        mag = torch.zeros(n, H, dtype=torch.float64).index_add_(0, seg, terms.abs())
+        got = aggr[: n * H].view(n, H).double().cpu()
+        err = (got - ref).abs()
+        bound = 2.0 ** -8 * ref.abs() + 1e-5 * mag + 1e-30
+        assert bool((err <= bound).all()), f"aggregate off: max excess {float((err - bound).max()):.3e}"
+        worst = max(worst, float((err / (ref.abs() + mag * 1e-3 + 1e-30)).max()))
+    return worst
+
+
+@pytest.mark.parametrize("graph", ["corner", "dense", "cylinder"])
+def test_edge_side_aggregate_equals_fp64_sum_of_terms(graph, monkeypatch):
+    n, ei = {"corner": _corner_graph, "dense": lambda: _random_graph(400, 24000, 5), "cylinder": _cylinder}[graph]()
+    e = ei.shape[1]
+    for mode in ("1", "0"):
+        *_, seen, scales, _ = _run(n, ei, mode, monkeypatch, record=True)
+        w = _check_aggregates(seen, scales, n, e)
+        print(f"{graph} MGN_EDGE_AGG={mode}: worst relative aggregate error {w:.2e}")
+
+
+@pytest.mark.parametrize("graph", ["corner", "dense"])
+def test_edge_side_aggregation_model_vs_fp64(graph, monkeypatch):
+    """Forward and every gradient with the edge-side aggregation within 2 x autocast's distance to fp64."""
+    n, ei = {"corner": _corner_graph, "dense": lambda: _random_graph(400, 24000, 5)}[graph]()
+    mp = 3
+    y, gx, grads, _, _, (x, ea, gy) = _run(n, ei, "1", monkeypatch, mp=mp)
+    torch.manual_seed(0)
+    ref = O.OracleEPD(mp, 11, 3, 2, H)
+    rp = dict(ref.named_parameters())
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in rp.items()}
+    x64 = x.double().requires_grad_(True)
+    y64 = O.encode_process_decode(x64, ei, ea.double(), p64, mp)
+    (y64 * gy.double()).sum().backward()
+    pac = {k: v.detach().clone().requires_grad_(True) for k, v in rp.items()}
+    xac = x.clone().requires_grad_(True)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        yac = O.encode_process_decode(xac, ei, ea, pac, mp)
+    (yac.float() * gy).sum().backward()
+    assert relerr(y, y64) <= 2 * relerr(yac, y64), (relerr(y, y64), relerr(yac, y64))
+    assert relerr(gx, x64.grad) <= max(1e-2, 2 * relerr(xac.grad, x64.grad))
+    for k, g in grads.items():
+        assert torch.isfinite(g).all(), k
+        assert relerr(g, p64[k].grad) <= max(1e-2, 2 * relerr(pac[k].grad, p64[k].grad)), k
+
+
+def test_edge_side_aggregation_auto_threshold(monkeypatch):
+    """auto: on exactly when E >= 16 N (chained bf16 h=128 blocks)."""
+    import ctypes
+
+    from graphphysics import _native as nat
+    from graphphysics.models import _engine
+    from graphphysics.models.processors import EncodeProcessDecode
+
+    monkeypatch.delenv("MGN_EDGE_AGG", raising=False)
+    m = EncodeProcessDecode(1, 11, 3, 2, H, compute_dtype=torch.bfloat16).to(DEV)
+    pw = m._get_plan().packed(DEV, nat.MGN_BF16)
+    de, dn = pw.descs[3], pw.descs[4]
+    for n, e, on in ((100, 1600, True), (100, 1599, False), (1000, 5760, False)):
+        topo = _engine.get_topology(torch.randint(0, n, (2, e), device=DEV), n)
+        sb = nat.lib().mgn_block_forward_scratch_bytes(ctypes.byref(topo.struct), ctypes.byref(de), ctypes.byref(dn))
+        assert (sb > 0) == on, (n, e, sb)
