@@ -387,17 +387,24 @@ __device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64
     const bool first = m == 0 || dprev != di;
     const bool last = m == 15 || dnext != di;
     const int nb0 = __shfl(nb, lane & 48);  // lane 0 of this DPP row: the previous tile's last dst
-    int rs = 0;                             // first lane of this lane's run
     if (__builtin_amdgcn_ballot_w64(first) == 0x0001000100010001ull) {
-        // one run: plain prefix sums (lane 15 ends with the total)
+        // one run (the common case at high in-degree): its total by the transposing 16-lane reduction —
+        // lane m < 4 ends with feature 16t + 4g + r4(m) of it — and 4-byte stores from those lanes
+        float k[8];
 #pragma unroll
-        for (int d = 1; d <= 8; d *= 2)
+        for (int t = 0; t < 8; ++t) k[t] = row16_sum4(v[t], m);
+        const int nb15 = __shfl(nb, (lane & 48) | 15);
+        if (tile * TR >= a.M) return;
+        const int r4 = 2 * (m & 1) + ((m >> 1) & 1);
+        float* dst = nb0 == di ? a.agg_head + tile * H : nb15 == di ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
+        if (m < 4) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    v[t][r] += __int_as_float(dpp_shr_i(__float_as_int(v[t][r]), d));
-    } else {
+            for (int t = 0; t < 8; ++t) dst[16 * t + 4 * g + r4] = k[t];
+        }
+        return;
+    }
+    int rs = 0;  // first lane of this lane's run
+    {
         rs = first ? m : 0;
 #pragma unroll
         for (int d = 1; d <= 8; d *= 2) rs = max(rs, dpp_shr_i(rs, d));
