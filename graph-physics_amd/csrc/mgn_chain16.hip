@@ -379,8 +379,19 @@ __device__ __forceinline__ int dpp_shr_i(int v, int d) {
         default: return __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
     }
 }
+#ifndef MGN_EAGG_ABL
+#define MGN_EAGG_ABL 0  // diagnostics builds only (results wrong): 1 no partial stores, 2 no reduction, 4 nothing
+#endif
 __device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64_t tile, int lane,
                                                const ChainFwdArgs& a) {
+    if (MGN_EAGG_ABL & 4) return;
+    if (MGN_EAGG_ABL & 2) {
+        if ((lane & 15) == 15 && tile * TR < a.M && !(MGN_EAGG_ABL & 1)) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(a.agg_full + (int64_t)di * H + 16 * t + 4 * (lane >> 4)) = v[t];
+        }
+        return;
+    }
     const int m = lane & 15, g = lane >> 4;
     const int dprev = __builtin_amdgcn_update_dpp(-1, di, 0x111, 0xF, 0xF, false);  // row_shr:1 (m = 0 keeps -1)
     const int dnext = __builtin_amdgcn_update_dpp(-1, di, 0x101, 0xF, 0xF, false);  // row_shl:1 (m = 15 keeps -1)
@@ -397,7 +408,7 @@ __device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64
         if (tile * TR >= a.M) return;
         const int r4 = 2 * (m & 1) + ((m >> 1) & 1);
         float* dst = nb0 == di ? a.agg_head + tile * H : nb15 == di ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
-        if (m < 4) {
+        if (m < 4 && !(MGN_EAGG_ABL & 1)) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) dst[16 * t + 4 * g + r4] = k[t];
         }
@@ -424,6 +435,7 @@ __device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64
     const bool sb = rs == 0 && nb0 == di;  // the run holds lane 0 and continues from the previous tile
     const bool ca = m == 15 && nb == di;   // it continues into the next tile
     float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
+    if (MGN_EAGG_ABL & 1) return;
 #pragma unroll
     for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(dst + 16 * t + 4 * g) = v[t];
 }
