@@ -364,80 +364,82 @@ __device__ __forceinline__ int load_nb(const ChainFwdArgs& a, int64_t tile, int 
     return ok ? v : -1;
 }
 
-// EdgeAgg: the messages v (this lane's row m, features 16t + 4g + r; 0 for rows >= M) summed over each
-// run of equal dst among the tile's 16 rows — a segmented inclusive scan over the 16 lanes of each DPP row
-// (row_shr 1, 2, 4, 8; a tile of one run, the common case at high in-degree, skips the segment tests)
-// — then the run's last lane stores its sum: a segment that starts and ends in this tile into
-// agg_full[dst], the run continuing from the previous tile into agg_head[tile], the one continuing
-// into the next tile into agg_tail[tile] (rows sorted by dst: at most one of each per tile). Fixed
-// order: deterministic; the node forward adds the partial rows of a segment in tile order.
-__device__ __forceinline__ int dpp_shr_i(int v, int d) {
-    switch (d) {
-        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
-        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
-        case 4: return __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
-        default: return __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
-    }
-}
+// EdgeAgg: the per-edge terms v = z / q (this lane's row m, features 16t + 4g + r; the fp32 z the output
+// is made of — the RMSNorm scale s multiplies the sum in the node forward) summed over each run of equal
+// dst among the tile's 16 rows, and the sum stored as one fp32 row: a segment that starts and ends in this
+// tile into agg_full[dst], the run continuing from the previous tile into agg_head[tile], the one
+// continuing into the next tile into agg_tail[tile] (rows sorted by dst: at most one of each per tile).
+// The runs are found from a ballot of lanes whose dst differs from the previous row's (wave-uniform: the
+// four DPP rows of lane groups g hold the same rows), and each run is reduced over the 16 lanes with a
+// transposing butterfly — xor 1 and xor 2 (quad_perm) exchange half of the lane's values each, rotations
+// by 4 and 8 add the quads — after which lane m < 4 holds the run's features 16t + 4g .. +3 for t = m and
+// m + 4: two 16-byte stores per lane, one 512-byte row per run (store instructions, not bytes, are what
+// this kernel pays for). Fixed order: deterministic; the node forward adds a segment's rows in tile order.
 #ifndef MGN_EAGG_ABL
-#define MGN_EAGG_ABL 0  // diagnostics builds only (results wrong): 1 no partial stores, 2 no reduction, 4 nothing
+#define MGN_EAGG_ABL 0  // diagnostics builds only (results wrong): 1 no partial stores, 4 nothing
 #endif
-__device__ __forceinline__ void edge_agg_store(f4 (&v)[8], int di, int nb, int64_t tile, int lane,
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// one run (lanes [r0, r1] of each row; all = the whole tile) reduced as above into u[k] (t = 4k + (m & 3))
+template <bool ALL>
+__device__ __forceinline__ void run_reduce(const f4 (&v)[8], int m, int r0, int r1, f4 (&u)[2]) {
+    const bool in = ALL || (m >= r0 && m <= r1);
+    const bool o1 = m & 1, o2 = (m >> 1) & 1;
+    f4 u1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float a0 = in ? v[2 * j][r] : 0.f, a1 = in ? v[2 * j + 1][r] : 0.f;
+            u1[j][r] = (o1 ? a1 : a0) + dpp_f<0xB1>(o1 ? a0 : a1);  // xor 1: t parity
+        }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float b0 = u1[2 * k][r], b1 = u1[2 * k + 1][r];
+            float w = (o2 ? b1 : b0) + dpp_f<0x4E>(o2 ? b0 : b1);  // xor 2: t bit 1
+            w += dpp_f<0x124>(w);                                    // row_ror:4
+            u[k][r] = w + dpp_f<0x128>(w);                           // row_ror:8
+        }
+}
+__device__ __forceinline__ void edge_agg_store(const f4 (&v)[8], int di, int nb, int64_t tile, int lane,
                                                const ChainFwdArgs& a) {
     if (MGN_EAGG_ABL & 4) return;
-    if (MGN_EAGG_ABL & 2) {
-        if ((lane & 15) == 15 && tile * TR < a.M && !(MGN_EAGG_ABL & 1)) {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(a.agg_full + (int64_t)di * H + 16 * t + 4 * (lane >> 4)) = v[t];
-        }
-        return;
-    }
     const int m = lane & 15, g = lane >> 4;
     const int dprev = __builtin_amdgcn_update_dpp(-1, di, 0x111, 0xF, 0xF, false);  // row_shr:1 (m = 0 keeps -1)
-    const int dnext = __builtin_amdgcn_update_dpp(-1, di, 0x101, 0xF, 0xF, false);  // row_shl:1 (m = 15 keeps -1)
-    const bool first = m == 0 || dprev != di;
-    const bool last = m == 15 || dnext != di;
-    const int nb0 = __shfl(nb, lane & 48);  // lane 0 of this DPP row: the previous tile's last dst
-    if (__builtin_amdgcn_ballot_w64(first) == 0x0001000100010001ull) {
-        // one run (the common case at high in-degree): its total by the transposing 16-lane reduction —
-        // lane m < 4 ends with feature 16t + 4g + r4(m) of it — and 4-byte stores from those lanes
-        float k[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) k[t] = row16_sum4(v[t], m);
-        const int nb15 = __shfl(nb, (lane & 48) | 15);
-        if (tile * TR >= a.M) return;
-        const int r4 = 2 * (m & 1) + ((m >> 1) & 1);
-        float* dst = nb0 == di ? a.agg_head + tile * H : nb15 == di ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
-        if (m < 4 && !(MGN_EAGG_ABL & 1)) {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) dst[16 * t + 4 * g + r4] = k[t];
+    // run starts of row 0 (the other rows are the same rows); wave-uniform
+    uint32_t starts = (uint32_t)__builtin_amdgcn_ballot_w64(m == 0 || dprev != di) & 0xFFFFu;
+    const int nb0 = __builtin_amdgcn_readlane(nb, 0), nb15 = __builtin_amdgcn_readlane(nb, 15);
+    const bool live = tile * TR < a.M;
+    auto put = [&](const f4 (&u)[2], int d, bool first, bool last) {
+        const bool sb = first && nb0 == d, ca = last && nb15 == d;
+        float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)d * H;
+        if (m < 4 && live && !(MGN_EAGG_ABL & 1)) {
+            *reinterpret_cast<f4*>(dst + 16 * m + 4 * g) = u[0];
+            *reinterpret_cast<f4*>(dst + 16 * (m + 4) + 4 * g) = u[1];
         }
+    };
+    if (starts == 1u) {  // one run (the common case at high in-degree)
+        f4 u[2];
+        run_reduce<true>(v, m, 0, 15, u);
+        put(u, __builtin_amdgcn_readfirstlane(di), true, true);
         return;
     }
-    int rs = 0;  // first lane of this lane's run
-    {
-        rs = first ? m : 0;
-#pragma unroll
-        for (int d = 1; d <= 8; d *= 2) rs = max(rs, dpp_shr_i(rs, d));
-#pragma unroll
-        for (int d = 1; d <= 8; d *= 2) {
-            const bool ok = m - d >= rs;
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float sh = __int_as_float(dpp_shr_i(__float_as_int(v[t][r]), d));
-                    v[t][r] += ok ? sh : 0.f;
-                }
-        }
+    int r0 = 0;
+    starts &= ~1u;
+#pragma unroll 1
+    while (true) {
+        const int r1 = starts ? __builtin_ctz(starts) - 1 : 15;  // wave-uniform run [r0, r1]
+        f4 u[2];
+        run_reduce<false>(v, m, r0, r1, u);
+        put(u, __builtin_amdgcn_readlane(di, r0), r0 == 0, r1 == 15);
+        if (!starts) break;
+        r0 = r1 + 1;
+        starts &= starts - 1;
     }
-    if (!last || tile * TR >= a.M) return;
-    const bool sb = rs == 0 && nb0 == di;  // the run holds lane 0 and continues from the previous tile
-    const bool ca = m == 15 && nb == di;   // it continues into the next tile
-    float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)di * H;
-    if (MGN_EAGG_ABL & 1) return;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) *reinterpret_cast<f4*>(dst + 16 * t + 4 * g) = v[t];
 }
 
 // SAVE = false: inference (no autograd): only z and rden (the node MLP's aggregation inputs) are
@@ -537,30 +539,25 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         if (g == 0 && row < a.M) a.rden_save[row] = q;
         store_rows<ZP2>(acc, scr, a.z_save, tile, a.M, lane);
         STAMP(5);
-        bf16x4 zb[8];  // EAGG: the bf16 z the messages are made of (the node forward's terms)
-        if (EAGG) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) zb[t] = bf16x4{(__bf16)acc[t][0], (__bf16)acc[t][1], (__bf16)acc[t][2], (__bf16)acc[t][3]};
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[t][r] *= rq;  // z / q: the output's term and (EAGG) the message
+        if (EAGG) {
+            if (row >= a.M) {  // clamped rows of the last tile (same dst as the last real row) add 0
+#pragma unroll
+                for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+            }
+            edge_agg_store(acc, di, nb, tile, lane, a);
         }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                acc[t][r] = fmaf(s[r], acc[t][r] * rq, (float)in.eb[t >> 1][4 * (t & 1) + r]);
+                acc[t][r] = fmaf(s[r], acc[t][r], (float)in.eb[t >> 1][4 * (t & 1) + r]);
         }
         store_rows(acc, scr, a.out, tile, a.M, lane);
-        if (EAGG) {
-            // the messages s ⊙ z / q as the node forward's aggregation takes them (bf16 z, 1/q, then s)
-            const bool live = row < a.M;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[t][r] = live ? s[r] * ((float)zb[t][r] * rq) : 0.f;
-            }
-            edge_agg_store(acc, di, nb, tile, lane, a);
-        }
         STAMP(6);
 #pragma unroll
         for (int s = 0; s < 4; ++s) pin(nxt.eb[s]);
@@ -885,8 +882,9 @@ __device__ __forceinline__ void node_proj_partner(const ChainNodeFwdArgs& a, int
 }
 
 // SAVE = false: inference — no aggregate, R8, mask, z or rden saves
-// EAGG (round 6): the aggregate from the edge forward's per-tile partial rows (edge_agg_store) instead of
-// every in-edge's z: agg_full[v], or agg_tail[tb] + agg_head[tb + 1] + ... + agg_head[te] in tile order
+// EAGG (round 6): the aggregate from the edge forward's per-tile partial rows of z/q (edge_agg_store)
+// instead of every in-edge's z: s ⊙ (agg_full[v], or agg_tail[tb] + agg_head[tb + 1] + ... + agg_head[te]
+// in tile order)
 template <bool SAVE, bool EAGG = false>
 __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -944,6 +942,9 @@ __global__ __launch_bounds__(NW * 64) void chain16_node_fwd_kernel(ChainNodeFwdA
                         for (int t = 0; t < 8; ++t) agg[t] += h1[t];
                     }
                 }
+                // the edge RMSNorm scale s, factored out of the partial sums (Σ s ⊙ z/q = s ⊙ Σ z/q)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) agg[t] *= *reinterpret_cast<const f4*>(a.agg_scale + 16 * t + 4 * g);
             }
             return;
         }
