@@ -379,8 +379,8 @@ __device__ __forceinline__ int load_nb(const ChainFwdArgs& a, int64_t tile, int 
 #define MGN_EAGG_ABL 0  // diagnostics builds only (results wrong): 1 no partial stores, 4 nothing
 #endif
 template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+__device__ __forceinline__ float dpp_f(float v) {  // within-row permutes only: every source lane is valid
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 // one run (lanes [r0, r1] of each row; all = the whole tile) reduced as above into u[k] (t = 4k + (m & 3))
 template <bool ALL>
@@ -409,12 +409,15 @@ __device__ __forceinline__ void edge_agg_store(const f4 (&v)[8], int di, int nb,
                                                const ChainFwdArgs& a) {
     if (MGN_EAGG_ABL & 4) return;
     const int m = lane & 15, g = lane >> 4;
+    // the last tile's clamped rows (row >= M) form a run of their own (dst -2) that is not stored
+    if (tile * TR + m >= a.M) di = -2;
     const int dprev = __builtin_amdgcn_update_dpp(-1, di, 0x111, 0xF, 0xF, false);  // row_shr:1 (m = 0 keeps -1)
     // run starts of row 0 (the other rows are the same rows); wave-uniform
     uint32_t starts = (uint32_t)__builtin_amdgcn_ballot_w64(m == 0 || dprev != di) & 0xFFFFu;
     const int nb0 = __builtin_amdgcn_readlane(nb, 0), nb15 = __builtin_amdgcn_readlane(nb, 15);
     const bool live = tile * TR < a.M;
     auto put = [&](const f4 (&u)[2], int d, bool first, bool last) {
+        if (d < 0) return;  // the padding run
         const bool sb = first && nb0 == d, ca = last && nb15 == d;
         float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)d * H;
         if (m < 4 && live && !(MGN_EAGG_ABL & 1)) {
@@ -543,13 +546,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         for (int t = 0; t < 8; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[t][r] *= rq;  // z / q: the output's term and (EAGG) the message
-        if (EAGG) {
-            if (row >= a.M) {  // clamped rows of the last tile (same dst as the last real row) add 0
-#pragma unroll
-                for (int t = 0; t < 8; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-            }
-            edge_agg_store(acc, di, nb, tile, lane, a);
-        }
+        if (EAGG) edge_agg_store(acc, di, nb, tile, lane, a);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
