@@ -72,6 +72,10 @@ struct ChainBwdArgs {
     float* dscale_part;         // [grid][128]
     __bf16* de;                 // [M][128] de_out + dZ0·W0a
     __bf16* dz0;                // [M][128] dZ0 row-major
+    // round 6, EdgeAgg in the backward: dZ0's dst-direction segment sums per tile run (node_grad's dP_i)
+    float* agg_full;
+    float* agg_head;
+    float* agg_tail;
 };
 
 // Node MLP (16-row chained kernels): in = [x ‖ aggr], aggr[v] = Σ_{k: dst(k)=v} s_e ⊙ z_k / q_k
@@ -161,9 +165,13 @@ int chain16_edge_wgrad_recompute(const mgn_mlp* m, const void* e, const void* pr
                                  hipStream_t st);
 // din2 / dout2 (p2 only): de_out read / de written in the pair layout (between the edge backwards of
 // consecutive processor blocks, mgn_block_backward_deferred2)
+// agg_scratch (optional, chain16_edge_agg_bytes(N, M)): also dZ0's dst-direction sums per tile run
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st, bool p2, bool din2 = false, bool dout2 = false);
+                          hipStream_t st, bool p2, bool din2 = false, bool dout2 = false, int64_t N = 0,
+                          void* agg_scratch = nullptr);
+// the EdgeAgg scratch's parts (full [N][128], head / tail [rows_pad(E)/16][128] fp32)
+void chain16_edge_agg_parts(void* scratch, int64_t N, int64_t E, float** full, float** head, float** tail);
 // dense MLP in_dim <= 32 -> 128 -> 128 -> 128 -> 128 + RMSNorm, bf16 (the encoders): 16-row chained
 // kernels with the generic DENSE save layout (ReLU masks: chained lane words)
 bool chain_dense_eligible(const mgn_mlp* m);

@@ -356,11 +356,11 @@ __device__ __forceinline__ void load_idx(const ChainFwdArgs& a, int64_t tile, in
 
 // EdgeAgg (round 6): the dst of the rows adjoining the tile — lane 0 gets row 16·tile − 1's, lane 15 row
 // 16·tile + 16's (-1 where there is none); the other lanes' values are unused
-__device__ __forceinline__ int load_nb(const ChainFwdArgs& a, int64_t tile, int lane) {
+__device__ __forceinline__ int load_nb(const int32_t* dst, int64_t M, int64_t tile, int lane) {
     const int m = lane & 15;
     const int64_t r = m == 0 ? tile * TR - 1 : tile * TR + TR;
-    const bool ok = r >= 0 && r < a.M && (m == 0 || m == 15);
-    const int v = a.proj_i[ok ? r : 0];
+    const bool ok = r >= 0 && r < M && (m == 0 || m == 15);
+    const int v = dst[ok ? r : 0];
     return ok ? v : -1;
 }
 
@@ -382,31 +382,36 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {  // within-row permutes only: every source lane is valid
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// one run (lanes [r0, r1] of each row; all = the whole tile) reduced as above into u[k] (t = 4k + (m & 3))
-template <bool ALL>
-__device__ __forceinline__ void run_reduce(const f4 (&v)[8], int m, int r0, int r1, f4 (&u)[2]) {
+// one run (lanes [r0, r1] of each row; all = the whole tile) reduced as above: half h of the lane's values
+// (t = 4h .. 4h + 3) into u (t = 4h + (m & 3)); halves one at a time keep the temporaries at 12 registers
+template <bool ALL, class V>
+__device__ __forceinline__ f4 run_reduce_half(const V& v, int h, int m, int r0, int r1) {
     const bool in = ALL || (m >= r0 && m <= r1);
     const bool o1 = m & 1, o2 = (m >> 1) & 1;
-    f4 u1[4];
+    f4 u1[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const float a0 = in ? v[2 * j][r] : 0.f, a1 = in ? v[2 * j + 1][r] : 0.f;
+            const float a0 = in ? v(4 * h + 2 * j, r) : 0.f, a1 = in ? v(4 * h + 2 * j + 1, r) : 0.f;
             u1[j][r] = (o1 ? a1 : a0) + dpp_f<0xB1>(o1 ? a0 : a1);  // xor 1: t parity
         }
+    f4 u;
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float b0 = u1[2 * k][r], b1 = u1[2 * k + 1][r];
-            float w = (o2 ? b1 : b0) + dpp_f<0x4E>(o2 ? b0 : b1);  // xor 2: t bit 1
-            w += dpp_f<0x124>(w);                                    // row_ror:4
-            u[k][r] = w + dpp_f<0x128>(w);                           // row_ror:8
-        }
+    for (int r = 0; r < 4; ++r) {
+        float w = (o2 ? u1[1][r] : u1[0][r]) + dpp_f<0x4E>(o2 ? u1[0][r] : u1[1][r]);  // xor 2: t bit 1
+        w += dpp_f<0x124>(w);                                                            // row_ror:4
+        u[r] = w + dpp_f<0x128>(w);                                                      // row_ror:8
+    }
+    return u;
 }
-__device__ __forceinline__ void edge_agg_store(const f4 (&v)[8], int di, int nb, int64_t tile, int lane,
-                                               const ChainFwdArgs& a) {
+struct AggOut {
+    float *full, *head, *tail;
+    int64_t M;
+};
+// v(t, r): the lane's term of feature 16t + 4g + r
+template <class V>
+__device__ __forceinline__ void edge_agg_store(const V& v, int di, int nb, int64_t tile, int lane, const AggOut& a) {
     if (MGN_EAGG_ABL & 4) return;
     const int m = lane & 15, g = lane >> 4;
     // the last tile's clamped rows (row >= M) form a run of their own (dst -2) that is not stored
@@ -416,19 +421,20 @@ __device__ __forceinline__ void edge_agg_store(const f4 (&v)[8], int di, int nb,
     uint32_t starts = (uint32_t)__builtin_amdgcn_ballot_w64(m == 0 || dprev != di) & 0xFFFFu;
     const int nb0 = __builtin_amdgcn_readlane(nb, 0), nb15 = __builtin_amdgcn_readlane(nb, 15);
     const bool live = tile * TR < a.M;
-    auto put = [&](const f4 (&u)[2], int d, bool first, bool last) {
-        if (d < 0) return;  // the padding run
+    auto dst_of = [&](int d, bool first, bool last) -> float* {
         const bool sb = first && nb0 == d, ca = last && nb15 == d;
-        float* dst = sb ? a.agg_head + tile * H : ca ? a.agg_tail + tile * H : a.agg_full + (int64_t)d * H;
-        if (m < 4 && live && !(MGN_EAGG_ABL & 1)) {
-            *reinterpret_cast<f4*>(dst + 16 * m + 4 * g) = u[0];
-            *reinterpret_cast<f4*>(dst + 16 * (m + 4) + 4 * g) = u[1];
-        }
+        return sb ? a.head + tile * H : ca ? a.tail + tile * H : a.full + (int64_t)d * H;
     };
+    const bool st = m < 4 && live && !(MGN_EAGG_ABL & 1);
     if (starts == 1u) {  // one run (the common case at high in-degree)
-        f4 u[2];
-        run_reduce<true>(v, m, 0, 15, u);
-        put(u, __builtin_amdgcn_readfirstlane(di), true, true);
+        const int d = __builtin_amdgcn_readfirstlane(di);
+        if (d < 0) return;
+        float* dst = dst_of(d, true, true);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const f4 u = run_reduce_half<true>(v, h, m, 0, 15);
+            if (st) *reinterpret_cast<f4*>(dst + 16 * (m + 4 * h) + 4 * g) = u;
+        }
         return;
     }
     int r0 = 0;
@@ -436,9 +442,15 @@ __device__ __forceinline__ void edge_agg_store(const f4 (&v)[8], int di, int nb,
 #pragma unroll 1
     while (true) {
         const int r1 = starts ? __builtin_ctz(starts) - 1 : 15;  // wave-uniform run [r0, r1]
-        f4 u[2];
-        run_reduce<false>(v, m, r0, r1, u);
-        put(u, __builtin_amdgcn_readlane(di, r0), r0 == 0, r1 == 15);
+        const int d = __builtin_amdgcn_readlane(di, r0);
+        if (d >= 0) {  // (the padding run is not stored)
+            float* dst = dst_of(d, r0 == 0, r1 == 15);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const f4 u = run_reduce_half<false>(v, h, m, r0, r1);
+                if (st) *reinterpret_cast<f4*>(dst + 16 * (m + 4 * h) + 4 * g) = u;
+            }
+        }
         if (!starts) break;
         r0 = r1 + 1;
         starts &= starts - 1;
@@ -468,7 +480,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
     In16 nxt;
     int di, dj, nb = -1;
     load_idx(a, min(tile, last), lane, di, dj);
-    if (EAGG) nb = load_nb(a, min(tile, last), lane);
+    if (EAGG) nb = load_nb(a.proj_i, a.M, min(tile, last), lane);
     load_e(nxt, a, min(tile, last), lane);
     stage16<4, NWK * 64>(W, a.wpack, a.woff, a.wks, false);
     for (int i = threadIdx.x; i < 5 * H; i += NWK * 64) vec[i] = i < 4 * H ? a.bias[i / H][i % H] : a.scale[i - 4 * H];
@@ -493,7 +505,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         }
         int ndi, ndj, nnb = -1;
         load_idx(a, min(tile + stride, last), lane, ndi, ndj);
-        if (EAGG) nnb = load_nb(a, min(tile + stride, last), lane);
+        if (EAGG) nnb = load_nb(a.proj_i, a.M, min(tile + stride, last), lane);
         load_e(nxt, a, min(tile + stride, last), lane);
         const int64_t row = tile * TR + m;
         f4 acc[8];
@@ -546,7 +558,9 @@ __global__ __launch_bounds__(NWK * 64) void chain16_fwd_kernel(ChainFwdArgs a) {
         for (int t = 0; t < 8; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[t][r] *= rq;  // z / q: the output's term and (EAGG) the message
-        if (EAGG) edge_agg_store(acc, di, nb, tile, lane, a);
+        if (EAGG)
+            edge_agg_store([&](int t, int r) { return acc[t][r]; }, di, nb, tile, lane,
+                           AggOut{a.agg_full, a.agg_head, a.agg_tail, a.M});
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const f4 s = *reinterpret_cast<const f4*>(vec + 4 * H + 16 * t + 4 * g);
@@ -631,7 +645,9 @@ __device__ __forceinline__ void pin_in(const S& in) {
 }
 
 // DOUT2: de in the pair layout (for the previous block's edge backward)
-template <bool ZD, int NWK, bool P2, bool DIN2, bool DOUT2>
+// EAGG (round 6): also the dst-direction segment sums of dZ0 (node_grad's dP_i) per tile run, as the
+// forward's edge-side aggregation (edge_agg_store)
+template <bool ZD, int NWK, bool P2, bool DIN2, bool DOUT2, bool EAGG = false>
 __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __bf16* W = reinterpret_cast<__bf16*>(smem);
@@ -649,6 +665,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
     constexpr bool PGA = NWK < 12;  // three waves per SIMD: the gather is not prefetched (VGPR cap)
     const int gi0 = bidx(a, min(tile, last), lane);
     int gcur = gi0;
+    int nb = EAGG ? load_nb(a.gath_idx, a.M, min(tile, last), lane) : -1;
     stage16<4, NWK * 64>(W, a.wtpack, a.woff, a.wks, true);
     BIn16 nxt;
     bload<ZD, P2, DIN2, PGA>(nxt, a, min(tile, last), gi0, lane);
@@ -664,6 +681,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         ngi = bidx(a, min(tile + stride, last), lane);
         pin_in<PGA>(nxt);
         pin(ngi);
+        if (EAGG) pin(nb);
     }
     STAMP(0);
     for (; tile < a.ntiles; tile += stride) {
@@ -719,6 +737,7 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         STAMP(1);
         bload<ZD, P2, DIN2, PGA>(nxt, a, min(tile + stride, last), ngi, lane);
         const int ngi2 = bidx(a, min(tile + 2 * stride, last), lane);
+        const int nnb = EAGG ? load_nb(a.gath_idx, a.M, min(tile + stride, last), lane) : -1;
         bf16x8 B[4];
         to_operand(acc, B);
         STAMP(2);
@@ -726,12 +745,17 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         u32x2 dre[8];  // de_out of this tile again (cache-hot), for the layer-0 residual
 #pragma unroll
         for (int l = 3; l >= 1; --l) {
-            if (l == 1 && !ZD) load_acc_row<DIN2>(dre, a.dout + clamp_row(row, a.M) * H, g);
+            if (l == 1 && !ZD && !EAGG) load_acc_row<DIN2>(dre, a.dout + clamp_row(row, a.M) * H, g);
             // stores its B operand dZ_l (R8) under the MFMAs
             gemm16_st(acc, W, l, B, lane, scr, StoreDst{a.dz8 + (int64_t)l * a.RP * H, nullptr}, tile, a.M);
             STAMP(3);
             relu_mask(acc, mcur[l - 1]);
             to_operand(acc, B);
+            if (EAGG && l == 1) {  // dZ0's bf16 operand (node_grad's terms; rows >= M are 0), acc free meanwhile
+                edge_agg_store([&](int t, int r) { return (float)B[t >> 1][4 * (t & 1) + r]; }, gcur, nb, tile, lane,
+                               AggOut{a.agg_full, a.agg_head, a.agg_tail, a.M});
+                if (!ZD) load_acc_row<DIN2>(dre, a.dout + clamp_row(row, a.M) * H, g);  // after: fewer live registers
+            }
             STAMP(4);
         }
         // layer 0, e block: de = de_out + dZ0 · W0a (stores dZ0 row-major under the MFMAs, every
@@ -757,6 +781,10 @@ __global__ __launch_bounds__(NWK * 64) void chain16_bwd_kernel(ChainBwdArgs a) {
         pin(ngi2);
         gcur = ngi;
         ngi = ngi2;
+        if (EAGG) {
+            pin(nnb);
+            nb = nnb;
+        }
         STAMP(8);
     }
     STAMP_PRINT("bwd16");
@@ -1684,6 +1712,10 @@ static void agg_carve(void* scratch, int64_t N, int64_t E, float** full, float**
     *tail = reinterpret_cast<float*>(p);
 }
 
+void chain16_edge_agg_parts(void* scratch, int64_t N, int64_t E, float** full, float** head, float** tail) {
+    agg_carve(scratch, N, E, full, head, tail);
+}
+
 int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, const int32_t* pi, const int32_t* pj,
                          int64_t M, void* out, mgn_mlp_saved* sv, hipStream_t st, bool z_p2, bool save_act, int64_t N,
                          void* agg_scratch) {
@@ -1735,9 +1767,11 @@ int chain16_edge_forward(const mgn_mlp* m, const void* e, const void* proj, cons
 
 int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void* dout, const void* gath,
                           const int32_t* gath_idx, void* dz8, float* dscale_part, int* nparts, void* de, void* dz0,
-                          hipStream_t st, bool p2, bool din2, bool dout2) {
+                          hipStream_t st, bool p2, bool din2, bool dout2, int64_t N, void* agg_scratch) {
     ChainBwdArgs a;
     memset(&a, 0, sizeof(a));
+    const bool eagg = agg_scratch != nullptr;
+    if (eagg) agg_carve(agg_scratch, N, M, &a.agg_full, &a.agg_head, &a.agg_tail);
     a.dout = reinterpret_cast<const __bf16*>(dout);
     a.gath = reinterpret_cast<const __bf16*>(gath);
     a.gath_idx = gath_idx;
@@ -1761,7 +1795,14 @@ int chain16_edge_backward(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, 
     constexpr int nwk = edge_bwd_waves();
     MGN_REQUIRE(p2 || (!din2 && !dout2), "pair-layout de needs the chained node MLP");
     using K = void (*)(ChainBwdArgs);
-    const K kern = !p2    ? (dout ? (K)chain16_bwd_kernel<false, nwk, false, false, false>
+    MGN_REQUIRE(!eagg || p2, "backward edge-side aggregation: the chained node MLP only");
+    const K kern = eagg ? (!dout ? (dout2 ? (K)chain16_bwd_kernel<true, nwk, true, false, true, true>
+                                          : (K)chain16_bwd_kernel<true, nwk, true, false, false, true>)
+                           : din2 ? (dout2 ? (K)chain16_bwd_kernel<false, nwk, true, true, true, true>
+                                           : (K)chain16_bwd_kernel<false, nwk, true, true, false, true>)
+                                  : (dout2 ? (K)chain16_bwd_kernel<false, nwk, true, false, true, true>
+                                           : (K)chain16_bwd_kernel<false, nwk, true, false, false, true>))
+                   : !p2    ? (dout ? (K)chain16_bwd_kernel<false, nwk, false, false, false>
                                   : (K)chain16_bwd_kernel<true, nwk, false, false, false>)
                    : !dout ? (dout2 ? (K)chain16_bwd_kernel<true, nwk, true, false, true>
                                     : (K)chain16_bwd_kernel<true, nwk, true, false, false>)

@@ -3835,6 +3835,11 @@ struct CombArgs {
     int64_t N, RP;
     int32_t ldb, HP, NS;
     int32_t dx_pair;      // dx in the chained kernels' pair layout (bf16 h=128)
+    // round 6, edge-side aggregation: dP_i from the chained edge backward's per-tile run sums of dZ0
+    // (chain16_edge_backward agg_scratch): agg_full[v], or agg_tail[tb] + agg_head[tb + 1] + ... + agg_head[te]
+    const float* agg_full;
+    const float* agg_head;
+    const float* agg_tail;
 };
 
 template <class T, int H, int BM>
@@ -3951,7 +3956,26 @@ __global__ __launch_bounds__(MGN_THREADS) void node_grad_kernel(CombArgs a) {
         float acc[CH];
 #pragma unroll
         for (int e = 0; e < CH; ++e) acc[e] = 0.f;
-        if (s == 0 || !MGN_COMB_IDXPF) {
+        if (s == 0 && a.agg_full != nullptr) {
+            // target direction from the edge backward's partial rows (fp32), in tile order
+            if (kb < ke) {
+                const int tb = kb >> 4, te = (ke - 1) >> 4;
+                const float* p0 = tb == te ? a.agg_full + (row0 + r) * H + c : a.agg_tail + (int64_t)tb * H + c;
+#pragma unroll
+                for (int e = 0; e < CH; e += 4) {
+                    const f4 v = ld4(p0 + e);
+                    acc[e] = v[0], acc[e + 1] = v[1], acc[e + 2] = v[2], acc[e + 3] = v[3];
+                }
+#pragma unroll 1
+                for (int tt = tb + 1; tt <= te; ++tt) {
+#pragma unroll
+                    for (int e = 0; e < CH; e += 4) {
+                        const f4 v = ld4(a.agg_head + (int64_t)tt * H + c + e);
+                        acc[e] += v[0], acc[e + 1] += v[1], acc[e + 2] += v[2], acc[e + 3] += v[3];
+                    }
+                }
+            }
+        } else if (s == 0 || !MGN_COMB_IDXPF) {
 #pragma unroll 1
             for (int k = kb; k < ke; k += SG) {
                 int64_t src[SG];
@@ -4071,10 +4095,18 @@ int launch_proj(const mgn_mlp* edge, const void* x, int64_t N, float* proj, cons
 #endif
 template <class T, int H>
 int launch_node_grad(const mgn_mlp* edge, const mgn_topology* t, const void* dz0, const void* dx_part, void* dP8,
-                     void* dx, hipStream_t st, bool dx_pair = false) {
+                     void* dx, hipStream_t st, bool dx_pair = false, void* agg_scratch = nullptr) {
     constexpr int BM = MGN_COMB_BM, KSTEP = Mf<T>::KSTEP;
     CombArgs a;
     memset(&a, 0, sizeof(a));
+    if (agg_scratch) {
+        MGN_REQUIRE(!MGN_COMB_PAIR && H == 128 && sizeof(T) == 2, "edge-side aggregation: the chained bf16 blocks");
+        float *full, *head, *tail;
+        chain16_edge_agg_parts(agg_scratch, t->num_nodes, t->num_edges, &full, &head, &tail);
+        a.agg_full = full;
+        a.agg_head = head;
+        a.agg_tail = tail;
+    }
     a.dz0 = dz0;
     a.col_ptr = t->col_ptr;
     a.row_ptr = t->row_ptr;
@@ -4294,11 +4326,15 @@ size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* e
 // the node forward's 0.36 GB of z gathers per block. MGN_EDGE_AGG: "auto" (default: E >= 16 N), "1"
 // (every chained training block), "0" (never). The partial sums re-associate the fp32 aggregation (fixed
 // order, deterministic); the per-edge messages are the same bf16-z terms.
-static bool edge_agg_mode(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
+// bwd: the backward's use (the edge backward's dZ0 sums for node_grad's dP_i); MGN_EDGE_AGG "fwd" / "bwd"
+// turn one direction on alone (tests)
+static bool edge_agg_mode(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, bool bwd = false) {
     if (!(chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0)) return false;
     const char* v = getenv("MGN_EDGE_AGG");
     if (v && v[0] == '0') return false;
     if (v && v[0] == '1') return true;
+    if (v && !strcmp(v, "fwd")) return !bwd;
+    if (v && !strcmp(v, "bwd")) return bwd;
     return t->num_edges >= 16 * t->num_nodes;
 }
 
@@ -4445,7 +4481,7 @@ int mgn_block_forward_chain(const mgn_topology* t, const mgn_mlp* edge, const mg
 // nmlp: the node MLP's own (chained path: its dZ saves and slabs live until the block's single
 // weight-gradient launch at the end)
 struct BlockWs {
-    size_t mlp, nmlp, dxpart, daggr, dz0, dP8, total;
+    size_t mlp, nmlp, dxpart, daggr, dz0, dP8, agg, total;
 };
 
 static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node) {
@@ -4468,6 +4504,12 @@ static BlockWs block_ws_parts(const mgn_topology* t, const mgn_mlp* edge, const 
     o += align_up((size_t)rows_pad(t->num_edges) * H * es);  // chained path: padded rows written (zero)
     w.dP8 = o;
     o += align_up((size_t)2 * rows_pad(t->num_nodes) * H * es);
+    // edge-side aggregation of dZ0 (round 6, edge_agg_mode): the edge backward's per-tile run sums
+    w.agg = 0;
+    if (edge_agg_mode(t, edge, node, true)) {
+        w.agg = o;
+        o += align_up(chain16_edge_agg_bytes(t->num_nodes, t->num_edges));
+    }
     w.total = o;
     return w;
 }
@@ -4492,6 +4534,7 @@ struct BlockBwdCarve {
     float* part;     // edge slabs
     bool chained;    // bf16 h=128 register-chained MLPs (+ the bf16 ring)
     bool ring32;     // fp32 h=128 generic MLPs + the fp32 ring
+    void* agg;       // edge-side aggregation scratch (BlockWs.agg; nullptr: off)
 };
 
 // fp32 h=128 processor blocks (the reference's dtype): the node MLP's weight gradients join ONE fp32
@@ -4546,6 +4589,7 @@ static BlockBwdCarve block_bwd_carve(const mgn_topology* t, const mgn_mlp* edge,
     c.dz0 = w + wl.dz0;
     c.dP8 = w + wl.dP8;
     c.chained = chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0;
+    c.agg = wl.agg && c.chained ? w + wl.agg : nullptr;
     c.ring32 = !c.chained && ring_f32_eligible(t, edge, node);
     c.gen1 = !c.chained && !c.ring32 && gen1_eligible(t, edge, node);
     if (c.chained || c.ring32 || c.gen1) {
@@ -4652,7 +4696,7 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         // pair-layout z and d_aggr iff the node MLP is chained too (as in the forward)
         if (int r = chain16_edge_backward(edge, E, &saved->edge, de_out, c.d_aggr, t->csc_dst, c.dz8, c.dsp, &ntiles,
                                           de, c.dz0, st, chain_node_eligible(node), flags & MGN_BWD_DE_OUT_PAIR,
-                                          flags & MGN_BWD_DE_PAIR))
+                                          flags & MGN_BWD_DE_PAIR, t->num_nodes, c.agg))
             return r;
     } else if (E > 0) {
         if (int r = mlp_bwd_any(edge, MODE_EDGE, E, &saved->edge, de_out, dt, H, oe, c.dz8, c.dsp, st)) return r;
@@ -4663,7 +4707,7 @@ static int block_backward_data_impl(const mgn_topology* t, const mgn_mlp* edge, 
         MGN_DISPATCH_H(H, rc = (launch_node_grad<float, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st)))
     } else {
         MGN_DISPATCH_H(H, rc = (launch_node_grad<__bf16, HH>(edge, t, c.dz0, c.dx_part, c.dP8, dx, st,
-                                                              flags & MGN_BWD_DX_PAIR)))
+                                                              flags & MGN_BWD_DX_PAIR, c.agg)))
     }
     return rc;
 }

@@ -217,11 +217,13 @@ int mgn_block_forward_chain(const mgn_topology* t, const mgn_mlp* edge, const mg
                             const mgn_mlp* next_edge, void* next_ws, size_t next_ws_bytes,
                             int* next_proj_ready, mgn_stream_t stream);
 /* ABI v17: mgn_block_forward_chain with a scratch buffer for the edge-side aggregation. For graphs of
- * high in-degree (default E >= 16 N; env MGN_EDGE_AGG = 0 / 1 forces it off / on for chained blocks) the
- * training forward's edge-MLP kernel also sums each 16-edge tile's messages per run of equal target and
- * the node-MLP kernel adds those partial rows — a few per node — instead of re-reading every in-edge's
- * output row (reference layers.py:694-696, the sum aggregation; the fp32 sums re-associated, in a fixed
- * order). mgn_block_forward_scratch_bytes: the scratch it needs, 0 where it does not apply (then the call
+ * high in-degree (default E >= 16 N; env MGN_EDGE_AGG = 0 / 1 forces it off / on for chained blocks, "fwd"
+ * / "bwd" one direction only) the training forward's edge-MLP kernel also sums each 16-edge tile's
+ * messages per run of equal target and the node-MLP kernel adds those partial rows — a few per node —
+ * instead of re-reading every in-edge's output row (reference layers.py:694-696, the sum aggregation; the
+ * fp32 sums re-associated, in a fixed order). The backward does the same for the target-direction sums of
+ * the edge MLP's layer-0 gradient (the index backward of x[col]) inside mgn_block_backward*'s workspace
+ * (mgn_block_backward_workspace_bytes includes it). mgn_block_forward_scratch_bytes: the scratch it needs, 0 where it does not apply (then the call
  * is mgn_block_forward_chain). The scratch is free again when the call's work has run (one buffer can
  * serve every block of a stack). */
 size_t mgn_block_forward_scratch_bytes(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node);

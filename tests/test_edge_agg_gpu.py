@@ -12,6 +12,9 @@ re-reading every in-edge's z (reference layers.py:694-696, the sum aggregation).
   segmented-scan path);
 * the whole model (forward and every gradient) is no further from fp64 than 2 x PyTorch's bf16 autocast of
   the reference, like every bf16 check (tests/test_gpu_parity.py);
+* the backward's use (the edge backward's dZ0 sums per tile run for node_grad's dP_i, MGN_EDGE_AGG=bwd)
+  against the fused backward on the SAME forward: every gradient equal up to the re-associated fp32 sums
+  (rel-L2 <= 1e-2; a partial row dropped, doubled or misfiled moves the gradients of its nodes by O(1));
 * auto mode picks it exactly for E >= 16 N.
 """
 import numpy as np
@@ -228,6 +231,21 @@ def test_edge_side_aggregation_model_vs_fp64(graph, monkeypatch):
     print("\nwhole gradient (edge-side, fused, autocast):", e1, e0, eac)
     print("worst parameter (ratio, key, edge-side, fused, autocast):", sorted(worst)[-3:])
     assert e1 <= max(2 * eac, 1.25 * e0), (e1, e0, eac)
+
+
+@pytest.mark.parametrize("graph", ["corner", "dense", "cylinder"])
+def test_backward_edge_side_sums_match_fused_backward(graph, monkeypatch):
+    n, ei = {"corner": _corner_graph, "dense": lambda: _random_graph(400, 24000, 5), "cylinder": _cylinder}[graph]()
+    y0, gx0, g0, *_ = _run(n, ei, "0", monkeypatch)
+    y1, gx1, g1, *_ = _run(n, ei, "bwd", monkeypatch)
+    assert torch.equal(y0, y1)  # the forward is untouched
+    worst = max(relerr(g1[k], g0[k]) for k in g0)
+    print(f"\n{graph}: backward edge-side sums vs fused, worst parameter-gradient rel-L2 {worst:.2e}, "
+          f"x grad {relerr(gx1, gx0):.2e}")
+    assert relerr(gx1, gx0) <= 1e-2
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        assert relerr(g1[k], g0[k]) <= 1e-2, (k, relerr(g1[k], g0[k]))
 
 
 def test_edge_side_aggregation_auto_threshold(monkeypatch):
