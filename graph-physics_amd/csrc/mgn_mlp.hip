@@ -4326,8 +4326,10 @@ size_t mgn_block_forward_workspace_bytes(const mgn_topology* t, const mgn_mlp* e
 // the node forward's 0.36 GB of z gathers per block. MGN_EDGE_AGG: "auto" (default: E >= 16 N), "1"
 // (every chained training block), "0" (never). The partial sums re-associate the fp32 aggregation (fixed
 // order, deterministic); the per-edge messages are the same bf16-z terms.
-// bwd: the backward's use (the edge backward's dZ0 sums for node_grad's dP_i); MGN_EDGE_AGG "fwd" / "bwd"
-// turn one direction on alone (tests)
+// bwd: the backward's use (the edge backward's dZ0 sums for node_grad's dP_i) — measured at Cfg E
+// (profiles/r06_eagg_ab.txt): node_grad 145.5 -> 127.5 us but the edge backward 510 -> 533 us, so "auto"
+// keeps it off (the target-direction half of node_grad streams contiguous rows and was already cheap);
+// MGN_EDGE_AGG "1" turns both on, "fwd" / "bwd" one direction alone (tests, A/B)
 static bool edge_agg_mode(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, bool bwd = false) {
     if (!(chain_eligible(edge) && chain_node_eligible(node) && t->num_nodes > 0 && t->num_edges > 0)) return false;
     const char* v = getenv("MGN_EDGE_AGG");
@@ -4335,7 +4337,7 @@ static bool edge_agg_mode(const mgn_topology* t, const mgn_mlp* edge, const mgn_
     if (v && v[0] == '1') return true;
     if (v && !strcmp(v, "fwd")) return !bwd;
     if (v && !strcmp(v, "bwd")) return bwd;
-    return t->num_edges >= 16 * t->num_nodes;
+    return !bwd && t->num_edges >= 16 * t->num_nodes;
 }
 
 static int block_forward_impl(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp* node, const void* x,
