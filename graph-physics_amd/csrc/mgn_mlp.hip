@@ -2000,6 +2000,14 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 #ifndef MGN_F32C_SB
 #define MGN_F32C_SB 0  // 1: single-buffered images, 6-wave workgroups, two workgroups per CU (A/B builds)
 #endif
+// MGN_F32C_FLOW (round 6): the forward's per-layer workgroup barrier replaced by LDS counters — a wave
+// waits only for the image of the layer it is about to run (ready[l]); the last wave to finish reading an
+// image stages layer l+2 into it. Waves drift apart by up to a layer, so one wave's ReLU / mask / store
+// phase runs beside another's MFMAs on the same SIMD instead of the whole workgroup idling the MFMA pipe
+// in lock-step.
+#ifndef MGN_F32C_FLOW
+#define MGN_F32C_FLOW 0
+#endif
 constexpr int F32C_WAVES = MGN_F32C_SB ? 6 : 12;  // three waves per SIMD (168 VGPRs), 16 rows per wave
 constexpr int F32C_NBUF = MGN_F32C_SB ? 1 : 2;    // LDS chain images per workgroup
 #define F32C_BOUNDS __launch_bounds__(F32C_WAVES * 64, 3)
@@ -2107,6 +2115,15 @@ __device__ __forceinline__ void f32c_gemm(f4 (&acc)[8], const f4 (&x)[8], const 
     }
 }
 
+// LDS counters of the flow-synchronized form: done[l] waves finished reading layer l's image, ready[l]
+__device__ __forceinline__ void f32c_wait(const unsigned* f, unsigned target) {
+    for (unsigned n = 0; n < (1u << 26); ++n) {  // bounded: a correct schedule never comes near
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
     constexpr int H = 128;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2114,6 +2131,7 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
     float* const img1 = img0 + (F32C_NBUF - 1) * F32C_LAYER;
     float* const vec = img0 + F32C_NBUF * F32C_LAYER;  // [5][H]: biases b0..b3, RMSNorm scale (LDS: no VMEM loads
                                            // behind the saves' stores, which would wait for them)
+    unsigned* const flg = reinterpret_cast<unsigned*>(vec + 5 * 128);  // MGN_F32C_FLOW: done[4], ready[4]
     const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15;
     const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + (threadIdx.x >> 6);
     const int64_t row0 = tile * 16, row = row0 + ri;
@@ -2150,6 +2168,7 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
         const float* vp = vl == 0 ? a.bias[0] : vl == 1 ? a.bias[1] : vl == 2 ? a.bias[2] : vl == 3 ? a.bias[3] : a.scale;
         vec[i] = vp[i & (H - 1)];
     }
+    if (MGN_F32C_FLOW && threadIdx.x < 8) flg[threadIdx.x] = 0u;
     f32c_stage_wait();
     __syncthreads();
 #pragma unroll
@@ -2159,16 +2178,24 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
     const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
     const float* res = reinterpret_cast<const float*>(a.resid);
     f4 rv[8];
+    const int wave = threadIdx.x >> 6;
+    const float* pk2 = pk;  // MGN_F32C_FLOW: layer l's chain image at pk2 + (l - 1) * step + image offset
+    const int64_t pstep = linear_pack_elems(H, H, MGN_F32);
+    bool loader = false;    // MGN_F32C_FLOW: this wave staged layer l+2 and signals ready[l+2] after its V_l
 #pragma unroll 1
     for (int l = 0; l < 4; ++l) {
         const float* nxt = nullptr;
-        if (l < 3) {
+        if (MGN_F32C_FLOW) {
+            if (l == 0) f32c_stage(pk2 + chain_image_off(H, H), img1);  // layer 1, every wave's share
+            if (l >= 1) f32c_wait(flg + 4 + l, l == 1 ? F32C_WAVES : 1u);
+        } else if (l < 3) {
             // layer l+1's image streams into the other buffer during this layer's MFMAs (its readers,
             // layer l-1, passed the last barrier); single-buffered: after every wave's MFMAs
             nxt = pk + chain_image_off(H, H);
             if (F32C_NBUF == 2) f32c_stage(nxt, (l & 1) ? img0 : img1);
             pk += linear_pack_elems(H, H, MGN_F32);
-        } else {
+        }
+        if (l == 3) {
             // the residual lands during the last GEMM
 #pragma unroll
             for (int nt = 0; nt < 8; ++nt)
@@ -2180,6 +2207,20 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
         float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
         f32c_gemm(acc, x, (l & 1) ? img1 : img0, lane, (l > 0 && live) ? sv + r8 : nullptr);
         F32C_STAMP(1);
+        if (MGN_F32C_FLOW) {
+            // done reading layer l's image (its reads were consumed by the MFMAs): the last wave out
+            // stages layer l+2 into it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            unsigned old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(flg + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readfirstlane(old);
+            loader = l + 2 <= 3 && old == F32C_WAVES - 1;
+            if (loader) {
+                const float* src = pk2 + (int64_t)(l + 1) * pstep + chain_image_off(H, H);
+                float* img = (l & 1) ? img1 : img0;
+                for (int c = 0; c < F32C_LAYER / 256; ++c) glds16(src + c * 256 + lane * 4, img + c * 256);
+            }
+        }
         if (l < 3) {
             unsigned long long word = 0;
 #pragma unroll
@@ -2196,12 +2237,22 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
             // the tile's 32 ballot words of layer l: word nt*4 + r from lane nt*4 + r
             if (live && lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
             F32C_STAMP(2);
-            if (F32C_NBUF == 1) {
+            if (MGN_F32C_FLOW) {
+                f32c_stage_wait();  // this wave's share of layer 1 (l = 0), the image it staged (loader)
+                asm volatile("" ::: "memory");
+                if (lane == 0) {
+                    if (l == 0) __hip_atomic_fetch_add(flg + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (loader) __hip_atomic_store(flg + 4 + l + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                (void)wave;
+            } else {
+                if (F32C_NBUF == 1) {
+                    __syncthreads();
+                    f32c_stage(nxt, img0);
+                }
+                f32c_stage_wait();
                 __syncthreads();
-                f32c_stage(nxt, img0);
             }
-            f32c_stage_wait();
-            __syncthreads();
             F32C_STAMP(3);
         }
     }
@@ -2879,7 +2930,7 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
             !a.ablate) {
             const int grid = (int)cdiv64(rows_pad(M), 16 * F32C_WAVES);
             if (grid == 0) return 0;
-            const size_t lds = (F32C_NBUF * F32C_LAYER + 5 * H) * sizeof(float);
+            const size_t lds = (F32C_NBUF * F32C_LAYER + 5 * H) * sizeof(float) + (MGN_F32C_FLOW ? 32 : 0);
             if (int e = set_lds((const void*)edge_fwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_FWD_EDGE, st);
             hipLaunchKernelGGL(edge_fwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
