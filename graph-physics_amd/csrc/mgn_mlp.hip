@@ -2008,6 +2008,7 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 #ifndef MGN_F32C_FLOW
 #define MGN_F32C_FLOW 0
 #endif
+static_assert(!MGN_F32C_FLOW || !MGN_F32C_SB, "the flow-synchronized form needs the double-buffered images");
 constexpr int F32C_WAVES = MGN_F32C_SB ? 6 : 12;  // three waves per SIMD (168 VGPRs), 16 rows per wave
 constexpr int F32C_NBUF = MGN_F32C_SB ? 1 : 2;    // LDS chain images per workgroup
 #define F32C_BOUNDS __launch_bounds__(F32C_WAVES * 64, 3)
@@ -2297,6 +2298,7 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
     float* const img0 = reinterpret_cast<float*>(smem);
     float* const img1 = img0 + (F32C_NBUF - 1) * F32C_LAYER;
     float* const red = img0 + F32C_NBUF * F32C_LAYER;  // [F32C_WAVES][H] per-wave RMSNorm-scale partials
+    unsigned* const flg = reinterpret_cast<unsigned*>(red + F32C_WAVES * 128);  // MGN_F32C_FLOW: done[4], ready[4]
     const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15, wave = threadIdx.x >> 6;
     const int64_t tile = (int64_t)blockIdx.x * F32C_WAVES + wave;
     const int64_t row0 = tile * 16, row = row0 + ri;
@@ -2389,6 +2391,7 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
         if (ri == 0) *reinterpret_cast<f4*>(red + wave * H + 16 * nt + 4 * g) = dsc;
 #endif
     }
+    if (MGN_F32C_FLOW && threadIdx.x < 8) flg[threadIdx.x] = 0u;
     f32c_stage_wait();
     __syncthreads();
     F32C_STAMP(0);
@@ -2408,14 +2411,21 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
     // ---- layers 3..1: dZ_{l-1} = (dZ_l · W_l) ⊙ [A_{l-1} > 0]; then de_in = dout + dZ_0 · W0a
     f4 acc[8], dv[8];
     const float* dout = reinterpret_cast<const float*>(a.dout);
+    // MGN_F32C_FLOW: the transposed image of step j (layer 3 - j)
+    auto bimg = [&](int j) { return wt + off[3 - j] + chain_image_off(H, j == 3 ? a.Kpack0 : H); };
+    bool loader = false;
 #pragma unroll 1
     for (int i = 0; i < 4; ++i) {
         const int l = 3 - i;  // layer whose transposed weights this GEMM uses
         const float* nxt = nullptr;
-        if (i < 3) {
+        if (MGN_F32C_FLOW) {
+            if (i == 0) f32c_stage(bimg(1), img1);  // every wave's share
+            if (i >= 1) f32c_wait(flg + 4 + i, i == 1 ? F32C_WAVES : 1u);
+        } else if (i < 3) {
             nxt = wt + off[l - 1] + chain_image_off(H, l == 1 ? a.Kpack0 : H);
             if (F32C_NBUF == 2) f32c_stage(nxt, (i & 1) ? img0 : img1);
-        } else {
+        }
+        if (i == 3) {
             // de_in = dout + dZ_0·W0a: dout lands during the last GEMM
 #pragma unroll
             for (int nt = 0; nt < 8; ++nt)
@@ -2427,6 +2437,18 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
         f32c_gemm(acc, dz, (i & 1) ? img1 : img0, lane, live ? dz8 + (int64_t)l * a.RP * H + r8 : nullptr);
         F32C_STAMP(1);
         if (i == 3) break;
+        if (MGN_F32C_FLOW) {  // as the forward: the last wave out of this image stages step i+2's into it
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            unsigned old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(flg + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readfirstlane(old);
+            loader = i + 2 <= 3 && old == F32C_WAVES - 1;
+            if (loader) {
+                const float* src = bimg(i + 2);
+                float* img = (i & 1) ? img1 : img0;
+                for (int c = 0; c < F32C_LAYER / 256; ++c) glds16(src + c * 256 + lane * 4, img + c * 256);
+            }
+        }
         // ReLU masks of hidden layer l-1: word nt*4 + r of the tile, bit = lane
         const unsigned long long mine = l == 3 ? mw[2] : l == 2 ? mw[1] : mw[0];
 #pragma unroll
@@ -2438,12 +2460,21 @@ __global__ F32C_BOUNDS void edge_bwd_f32_chain_kernel(BwdArgs a) {
                 dz[nt][r] = ((wd >> lane) & 1ull) && valid ? acc[nt][r] : 0.f;
             }
         F32C_STAMP(2);
-        if (F32C_NBUF == 1) {
+        if (MGN_F32C_FLOW) {
+            f32c_stage_wait();
+            asm volatile("" ::: "memory");
+            if (lane == 0) {
+                if (i == 0) __hip_atomic_fetch_add(flg + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (loader) __hip_atomic_store(flg + 4 + i + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+            if (F32C_NBUF == 1) {
+                __syncthreads();
+                f32c_stage(nxt, img0);
+            }
+            f32c_stage_wait();
             __syncthreads();
-            f32c_stage(nxt, img0);
         }
-        f32c_stage_wait();
-        __syncthreads();
         F32C_STAMP(3);
     }
     if (valid) {
@@ -3057,7 +3088,7 @@ int launch_bwd(const mgn_mlp* m, int64_t M, const mgn_mlp_saved* sv, const void*
             al16(a.o1) && al16(a.o2) && al16(a.dscale_part) && BM == 32) {
             const int grid = (int)cdiv64(a.RP, 16 * F32C_WAVES);
             if (grid == 0) return 0;
-            const size_t lds = (F32C_NBUF * F32C_LAYER + F32C_WAVES * H) * sizeof(float);
+            const size_t lds = (F32C_NBUF * F32C_LAYER + F32C_WAVES * H) * sizeof(float) + (MGN_F32C_FLOW ? 32 : 0);
             if (int e = set_lds((const void*)edge_bwd_f32_chain_kernel, lds)) return e;
             ProfScope ps(PROF_BWD_EDGE, st);
             hipLaunchKernelGGL(edge_bwd_f32_chain_kernel, dim3(grid), dim3(F32C_WAVES * 64), lds, st, a);
