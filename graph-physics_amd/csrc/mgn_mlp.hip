@@ -2006,7 +2006,7 @@ __global__ __launch_bounds__(MGN_THREADS) void pack_kernel(const mgn_pack_job* j
 // phase runs beside another's MFMAs on the same SIMD instead of the whole workgroup idling the MFMA pipe
 // in lock-step.
 #ifndef MGN_F32C_FLOW
-#define MGN_F32C_FLOW 0
+#define MGN_F32C_FLOW 1
 #endif
 static_assert(!MGN_F32C_FLOW || !MGN_F32C_SB, "the flow-synchronized form needs the double-buffered images");
 constexpr int F32C_WAVES = MGN_F32C_SB ? 6 : 12;  // three waves per SIMD (168 VGPRs), 16 rows per wave
