@@ -681,15 +681,16 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 
     // ---- dY -> dZ_last (RMSNorm backward), chunks of 4 columns; CPR lanes per row
     {
-        const int CPR = cdiv(NO, 4);  // <= 32, divides 256 for NOUT in {H} or <= 16 rounded
+        const int CPR = cdiv(NO, 4);  // <= 64, divides 256 for NOUT in {H} or <= 16 rounded
         const int RPP = MGN_THREADS / CPR;  // rows per pass
         const int cc = (tid % CPR) * 4, rr = tid / CPR;
         f4 dsc = {0.f, 0.f, 0.f, 0.f};
         f4 s = {1.f, 1.f, 1.f, 1.f};
         if (a.has_norm) s = ld4u(a.scale + cc);
         // passes of RPP rows, 4 passes per batch: all loads of a batch are issued before use
-        constexpr int MAXP = BM / 8 > 4 ? BM / 8 : 4;
-        for (int p0 = 0; p0 < MAXP; p0 += 4) {
+        // batches of 4 passes until the tile's BM rows are covered (RPP = 4 at hidden 256: 4 batches of a
+        // 32-row tile; 8+ rows per pass below)
+        for (int p0 = 0; p0 * RPP < BM; p0 += 4) {
             f4 dy[4], z[4];
             float q[4];
             bool valid[4];
@@ -916,7 +917,8 @@ __global__ __launch_bounds__(MGN_THREADS) void mlp_bwd_kernel(BwdArgs a) {
 struct WgJob {
     int32_t layer, kb, n, k, kp, staged;  // staged: B operand re-gathered from seg[] through LDS
     int64_t w_off, b_off, act_off;        // b_off < 0: no bias for this job
-    int32_t zl, pad;                      // dZ operand = R8 block zl of dz8
+    int32_t zl;                           // dZ operand = R8 block zl of dz8
+    int32_t nb;                           // output-feature block: rows [nb*TW, nb*TW + TW) of dW (hidden > 128)
     // multi-MLP launches (WgArgs.multi): the job's own rows, operands, slabs and (staged) segment —
     // one launch then covers every weight gradient of a GraphNetBlock (edge MLP over edge rows, node
     // MLP and the edge W0's x blocks over node rows); blockIdx.x >= nchunks: idle workgroup
@@ -959,19 +961,27 @@ constexpr int WG_GROUPS = 2;
 #define MGN_WG_QUAD 1
 #endif
 
+// Output tile of a weight-gradient workgroup: TW x TW (TW = H up to 128). Hidden sizes above 128 (256:
+// h = 129..256 zero-padded) split every dW into 128 x 128 tiles — job (kb, nb) = input columns
+// [kb*TW, +TW) x output features [nb*TW, +TW) — so the h = 128 kernel's registers and LDS carry over.
+template <int H>
+constexpr int wg_tile() { return H > 128 ? 128 : H; }
+
 template <class T, int H>
 size_t wgrad_lds_bytes(bool staged) {
-    // re-gathered layer-0 input: [2][H][64 + pad] per group; bf16 R8 input: [2][8 octets][H] x 16 B
-    const size_t stage = staged ? (size_t)WG_GROUPS * 2 * H * (64 + 16 / sizeof(T)) * sizeof(T)
-                                : (sizeof(T) == 2 ? (size_t)WG_GROUPS * 2 * 8 * H * 16 : 0);
-    const size_t red = (size_t)(H * (H + 4) + H) * sizeof(float);  // canonical combine tile + bias row
+    constexpr int TW = wg_tile<H>();
+    // re-gathered layer-0 input: [2][TW][64 + pad] per group; bf16 R8 input: [2][8 octets][TW] x 16 B
+    const size_t stage = staged ? (size_t)WG_GROUPS * 2 * TW * (64 + 16 / sizeof(T)) * sizeof(T)
+                                : (sizeof(T) == 2 ? (size_t)WG_GROUPS * 2 * 8 * TW * 16 : 0);
+    const size_t red = (size_t)(TW * (TW + 4) + TW) * sizeof(float);  // canonical combine tile + bias row
     return stage > red ? stage : red;
 }
 
 template <class T, int H>
 __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgArgs a) {
     constexpr int VEC = Mf<T>::VEC, KSTEP = Mf<T>::KSTEP;
-    constexpr int NT = H / 16;
+    constexpr int TW = wg_tile<H>();            // output tile TW x TW (H: the dZ row width)
+    constexpr int NT = TW / 16;
     constexpr int SR = 64;                      // rows per LDS stage
     constexpr int CH = 16 / sizeof(T);          // elements per 16-byte chunk
     constexpr int LDT = SR + CH;                // LDS row = one input column over SR rows (+pad)
@@ -980,7 +990,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     // group and wave index wave-uniform (readfirstlane): the row loops below then run on scalar
     // counters, without exec-masked exits
     const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x / MGN_THREADS), tid = threadIdx.x % MGN_THREADS;
-    T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * H * LDT;  // this group's [2][H][LDT]
+    T* AT = reinterpret_cast<T*>(smem) + (size_t)grp * 2 * TW * LDT;  // this group's [2][TW][LDT]
     F32C_STAMP_DECL;
     const WgJob job = a.job[blockIdx.y];
     const bool multi = a.multi != 0;
@@ -1004,7 +1014,8 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     const bool active = mt0 < NT;
     const T* Z = reinterpret_cast<const T*>(dz8) + (int64_t)job.zl * RP * H;
     const T* X = reinterpret_cast<const T*>(act8) + job.act_off;
-    const int col0 = job.kb * H;
+    const int col0 = job.kb * TW;
+    const int n0 = job.nb * TW;  // first output feature (dZ column) of this tile
     const bool staged = job.staged != 0;
     bool kon[C::MTW];
 #pragma unroll
@@ -1052,7 +1063,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 for (int i = 0; i < C::NTW; ++i)
                     zq[q][i] = *reinterpret_cast<const f4*>(
                         reinterpret_cast<const float*>(Z) + (((mc + q * 16) >> 3) + (g4 >> 1)) * H * 8 +
-                        (int64_t)((nt0 + i) * 16 + (lane & 15)) * 8 + 4 * (g4 & 1));
+                        (int64_t)(n0 + (nt0 + i) * 16 + (lane & 15)) * 8 + 4 * (g4 & 1));
         };
         issue_x(r_begin + grp * SR);
         issue_z(r_begin + grp * SR);
@@ -1096,7 +1107,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
                 for (int i = 0; i < C::NTW; ++i)
-                    zn[ks][i] = ld_frag(Z + r8_index(mc + ks * KSTEP + VEC * (lane >> 4), (nt0 + i) * 16 + (lane & 15), H));
+                    zn[ks][i] = ld_frag(Z + r8_index(mc + ks * KSTEP + VEC * (lane >> 4), n0 + (nt0 + i) * 16 + (lane & 15), H));
         };
         issue_x(r_begin + grp * SR);
         issue_z(r_begin + grp * SR);
@@ -1131,10 +1142,10 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     auto no_b4 = [](int, int, int) { return f4{0.f, 0.f, 0.f, 0.f}; };  // bf16-only pipelines
     if (!staged && VEC == 8) {
         // R8 input: the 4 waves of a group all need the same 8 X fragments per k-step, so the
-        // group copies each stage once (SR/8 octets x H columns x 16 B, coalesced: in R8 an
+        // group copies each stage once (SR/8 octets x TW columns x 16 B, coalesced: in R8 an
         // octet's columns are contiguous) and the waves read their fragments from LDS (lanes 0-15
         // = 16 consecutive columns: conflict-free).
-        constexpr int ITEMS = (SR / 8) * H;
+        constexpr int ITEMS = (SR / 8) * TW;
         constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;
         u32x4* img = reinterpret_cast<u32x4*>(smem) + (size_t)grp * 2 * ITEMS;
         u32x4 nxt[PER];
@@ -1144,7 +1155,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
 #pragma unroll
                 for (int q = 0; q < PER; ++q) {
                     const int it = tid + q * MGN_THREADS;
-                    const int o = it / H, c = it % H;
+                    const int o = it / TW, c = it % TW;
                     const int cc = col0 + c < job.kp ? col0 + c : 0;
                     nxt[q] = *reinterpret_cast<const u32x4*>(X + r8_index(mc + 8 * (it < ITEMS ? o : 0), cc, job.kp));
                     if (col0 + c >= job.kp) nxt[q] = u32x4{0u, 0u, 0u, 0u};
@@ -1158,7 +1169,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             },
             [&](int par, int ks, int j) {
                 const u32x4* buf = img + (size_t)par * ITEMS;
-                return ld_frag(reinterpret_cast<const T*>(buf + (ks * (KSTEP / 8) + (lane >> 4)) * H + (mt0 + j) * 16 +
+                return ld_frag(reinterpret_cast<const T*>(buf + (ks * (KSTEP / 8) + (lane >> 4)) * TW + (mt0 + j) * 16 +
                                                           (lane & 15)));
             },
             no_b4);
@@ -1183,7 +1194,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 const int64_t m = m0 < r_end ? m0 : r_begin;
 #pragma unroll
                 for (int i = 0; i < C::NTW; ++i)
-                    fa[i] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(Z) + qidx(m, (nt0 + i) * 16 + fl, H));
+                    fa[i] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(Z) + qidx(m, n0 + (nt0 + i) * 16 + fl, H));
 #pragma unroll
                 for (int j = 0; j < C::MTW; ++j)
                     fb[j] = *reinterpret_cast<const f4*>(reinterpret_cast<const float*>(X) +
@@ -1230,7 +1241,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
         auto load = [&](int64_t m0, typename Mf<T>::frag (&fa)[C::NTW], typename Mf<T>::frag (&fb)[C::MTW]) {
             const int64_t mr = (m0 < r_end ? m0 : r_begin) + VEC * (lane >> 4);
 #pragma unroll
-            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, n0 + (nt0 + i) * 16 + (lane & 15), H));
             // unconditional loads (an inactive column block reads a valid column and is zeroed where
             // consumed): a load-or-zero join would again make the compiler copy the ring registers
             const int cz = (lane & 15) < job.kp ? (lane & 15) : 0;
@@ -1273,7 +1284,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             const int64_t mr = m0 + VEC * (lane >> 4);
             typename Mf<T>::frag fa[C::NTW], fb[C::MTW];
 #pragma unroll
-            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, (nt0 + i) * 16 + (lane & 15), H));
+            for (int i = 0; i < C::NTW; ++i) fa[i] = ld_frag(Z + r8_index(mr, n0 + (nt0 + i) * 16 + (lane & 15), H));
 #pragma unroll
             for (int j = 0; j < C::MTW; ++j)
                 fb[j] = kon[j] ? ld_frag(X + r8_index(mr, col0 + (mt0 + j) * 16 + (lane & 15), job.kp)) : zero;
@@ -1283,8 +1294,8 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 for (int j = 0; j < C::MTW; ++j) acc[i][j] = Mf<T>::mma(fa[i], fb[j], acc[i][j]);
             if (do_bias) bias_acc(fa);
         }
-    } else if (VEC == 8 && H == 128) {
-        if constexpr (VEC == 8 && H == 128) {
+    } else if (VEC == 8 && TW == 128) {
+        if constexpr (VEC == 8 && TW == 128) {
             // re-gathered layer-0 input, bf16 h=128: rows staged ROW-major (consecutive threads take
             // consecutive 16-byte chunks of one row: coalesced 256-byte row reads, one ds_write_b128
             // each) and the column-major B fragments read back with ds_read_b64_tr_b16 (two 4-row
@@ -1293,11 +1304,11 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
             // columns) conflict-free.
             const SrcSeg g = pick_seg(col0);
             const T* src = reinterpret_cast<const T*>(g.p) + (col0 - g.coff);
-            constexpr int CPR = H / 8;                        // 16-byte chunks per row
+            constexpr int CPR = TW / 8;                       // 16-byte chunks per row
             constexpr int ITEMS = SR * CPR;
             constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;
-            char* img = smem + (size_t)grp * 2 * SR * H * sizeof(T);
-            auto slot = [](int r, int ch) { return r * (H * (int)sizeof(T)) + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); };
+            char* img = smem + (size_t)grp * 2 * SR * TW * sizeof(T);
+            auto slot = [](int r, int ch) { return r * (TW * (int)sizeof(T)) + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); };
             u32x4 nxt[PER];
             pipeline(
                 [&](int64_t m0) {
@@ -1314,7 +1325,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                     }
                 },
                 [&](int par) {
-                    char* buf = img + (size_t)par * SR * H * sizeof(T);
+                    char* buf = img + (size_t)par * SR * TW * sizeof(T);
     #pragma unroll
                     for (int q = 0; q < PER; ++q) {
                         const int it = tid + q * MGN_THREADS;
@@ -1324,7 +1335,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 [&](int par, int ks, int j) {
                     typedef short s4 __attribute__((ext_vector_type(4)));
                     typedef __attribute__((address_space(3))) s4 lds_s4;
-                    const char* buf = img + (size_t)par * SR * H * sizeof(T);
+                    const char* buf = img + (size_t)par * SR * TW * sizeof(T);
                     const int i = lane & 15, q = i >> 2, p = i & 3;
                     const int r0 = ks * KSTEP + 8 * (lane >> 4) + q;
                     const int ch = (mt0 + j) * 2 + (p >> 1);
@@ -1337,12 +1348,12 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 no_b4);
         }
     } else {
-        // re-gathered layer-0 input: segment holding columns [col0, col0 + H) (segments are H
+        // re-gathered layer-0 input: segment holding columns [col0, col0 + TW) (segments are H
         // wide); consecutive lanes take consecutive ROWS of one 16-byte column chunk, so the
         // transposed LDS writes (column-major AT[col][row]) hit consecutive 2-byte slots.
         const SrcSeg g = pick_seg(col0);
         const T* src = reinterpret_cast<const T*>(g.p);
-        constexpr int ITEMS = SR * (H / CH);
+        constexpr int ITEMS = SR * (TW / CH);
         constexpr int PER = (ITEMS + MGN_THREADS - 1) / MGN_THREADS;  // 16-byte chunks per thread
         u32x4 nxt[PER];
         pipeline(
@@ -1360,7 +1371,7 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 }
             },
             [&](int par) {
-                T* buf = AT + (size_t)par * H * LDT;
+                T* buf = AT + (size_t)par * TW * LDT;
 #pragma unroll
                 for (int q = 0; q < PER; ++q) {
                     const int it = tid + q * MGN_THREADS;
@@ -1372,23 +1383,23 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 }
             },
             [&](int par, int ks, int j) {
-                const T* buf = AT + (size_t)par * H * LDT;
+                const T* buf = AT + (size_t)par * TW * LDT;
                 return ld_frag(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + ks * KSTEP + VEC * (lane >> 4));
             },
             [&](int par, int q, int j) {  // fp32 only: rows 16q + 4g .. +3 of the column
-                const T* buf = AT + (size_t)par * H * LDT;
+                const T* buf = AT + (size_t)par * TW * LDT;
                 return *reinterpret_cast<const f4*>(buf + (size_t)((mt0 + j) * 16 + (lane & 15)) * LDT + q * 16 +
                                                     4 * (lane >> 4));
             });
     }
     F32C_STAMP(0);
-    // Combine and store through a canonical [n][k] tile in LDS (row pitch H+4 floats: the four
+    // Combine and store through a canonical [n][k] tile in LDS (row pitch TW+4 floats: the four
     // 16-lane groups of an accumulator write land 16 banks apart): group 1 deposits its tile,
     // group 0 adds its own, then all 512 threads store the slab rows with coalesced 16-byte stores
     // (the per-lane accumulator layout holds 4 rows x 1 column: scalar stores 4 rows apart).
-    constexpr int LP = H + 4;
+    constexpr int LP = TW + 4;
     float* tile = reinterpret_cast<float*>(smem);
-    float* btile = tile + H * LP;
+    float* btile = tile + TW * LP;
     float bt[C::NTW];
 #pragma unroll
     for (int i = 0; i < C::NTW; ++i) {
@@ -1419,13 +1430,14 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
     if (grp == 0 && active) deposit(true);
     __syncthreads();
     float* part = part0 + (int64_t)blockIdx.x * G;
-    constexpr int C4 = H / 4;
+    constexpr int C4 = TW / 4;
     const bool vec = ((G | job.w_off | (int64_t)job.k) & 3) == 0;
-    for (int it = threadIdx.x; it < H * C4; it += MGN_THREADS * WG_GROUPS) {
-        const int n = it / C4, k4 = (it % C4) * 4;
+    for (int it = threadIdx.x; it < TW * C4; it += MGN_THREADS * WG_GROUPS) {
+        const int n = n0 + it / C4, k4 = (it % C4) * 4;
         const int kc = col0 + k4;
         if (n >= job.n || kc >= job.k) continue;
-        const f4 v = *reinterpret_cast<const f4*>(tile + n * LP + k4);
+        const int nl = n - n0;
+        const f4 v = *reinterpret_cast<const f4*>(tile + nl * LP + k4);
         float* dst = part + job.w_off + (int64_t)n * job.k + kc;
         if (vec && kc + 4 <= job.k) {
             *reinterpret_cast<f4*>(dst) = v;
@@ -1435,7 +1447,8 @@ __global__ __launch_bounds__(MGN_THREADS * WG_GROUPS) void mlp_wgrad_kernel(WgAr
                 if (kc + e < job.k) dst[e] = v[e];
         }
     }
-    if (job.b_off >= 0 && (int)threadIdx.x < job.n && (int)threadIdx.x < H) part[job.b_off + threadIdx.x] = btile[threadIdx.x];
+    if (job.b_off >= 0 && (int)threadIdx.x < job.n - n0 && (int)threadIdx.x < TW)
+        part[job.b_off + n0 + threadIdx.x] = btile[threadIdx.x];
     F32C_STAMP(1);
     if (blockIdx.y == 0) F32C_STAMP_PRINT("gwg");
 }
@@ -2880,9 +2893,9 @@ int check_mlp(const mgn_mlp* m) {
     MGN_REQUIRE(m != nullptr, "mlp descriptor is NULL");
     MGN_REQUIRE(m->n_layers >= 2 && m->n_layers <= MGN_MAX_LAYERS,
                 "The MLP must have at least 2 layers (input and output) and at most 8");
-    MGN_REQUIRE(m->hidden == 16 || m->hidden == 32 || m->hidden == 64 || m->hidden == 128,
-                "kernel width (mgn_mlp.hidden) must be 16, 32, 64 or 128; a model of another hidden size "
-                "<= 128 runs zero-padded to the next width with norm_dim = its true size");
+    MGN_REQUIRE(m->hidden == 16 || m->hidden == 32 || m->hidden == 64 || m->hidden == 128 || m->hidden == 256,
+                "kernel width (mgn_mlp.hidden) must be 16, 32, 64, 128 or 256; a model of another hidden size "
+                "<= 256 runs zero-padded to the next width with norm_dim = its true size");
     MGN_REQUIRE(m->norm_dim >= 0 && m->norm_dim <= m->out_dim, "norm_dim must be in [0, out_dim]");
     MGN_REQUIRE(m->in_dim >= 1, "in_dim must be >= 1");
     MGN_REQUIRE(m->out_dim == m->hidden || (m->out_dim >= 1 && m->out_dim <= 16),
@@ -3326,8 +3339,15 @@ int launch_ring(const RgArgs& r, hipStream_t st, int prof_kind = PROF_WGRAD_DENS
     return 0;
 }
 
+// jobs: the launch's job list (a.job is filled from it; more than fit one WgArgs — hidden > 128, whose
+// 128 x 128 tiles multiply the jobs — run as several launches over the same chunks and slabs)
 template <class T, int H>
-int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
+int launch_wgrad_kernel(WgArgs& a, const WgJob* jobs, int nj, int nchunks, hipStream_t st) {
+    constexpr int JMAX = (int)(sizeof(a.job) / sizeof(a.job[0]));
+    if constexpr (H <= 128) {
+        MGN_REQUIRE(nj <= JMAX, "too many weight-gradient jobs");
+        for (int j = 0; j < nj; ++j) a.job[j] = jobs[j];
+    }
     a.njobs = nj;
     if constexpr (H == 128) {
         RgArgs r;
@@ -3361,10 +3381,20 @@ int launch_wgrad_kernel(WgArgs& a, int nj, int nchunks, hipStream_t st) {
     auto fn = mlp_wgrad_kernel<T, H>;
     const size_t lds = wgrad_lds_bytes<T, H>(a.gathered != 0);
     if (int e = set_lds((const void*)fn, wgrad_lds_bytes<T, H>(true))) return e;
-    if (nchunks > 0 && nj > 0) {
+    if (nchunks <= 0 || nj <= 0) return 0;
+    if constexpr (H <= 128) {
         ProfScope ps(PROF_WGRAD_DENSE, st);
         hipLaunchKernelGGL(fn, dim3(nchunks, nj), dim3(MGN_THREADS * WG_GROUPS), lds, st, a);
         MGN_LAUNCH_CHECK();
+    } else {
+        for (int j0 = 0; j0 < nj; j0 += JMAX) {
+            const int n = nj - j0 < JMAX ? nj - j0 : JMAX;
+            for (int j = 0; j < n; ++j) a.job[j] = jobs[j0 + j];
+            a.njobs = n;
+            ProfScope ps(PROF_WGRAD_DENSE, st);
+            hipLaunchKernelGGL(fn, dim3(nchunks, n), dim3(MGN_THREADS * WG_GROUPS), lds, st, a);
+            MGN_LAUNCH_CHECK();
+        }
     }
     return 0;
 }
@@ -3390,33 +3420,39 @@ int launch_wgrad(const mgn_mlp* m, int64_t M, const void* act8, const void* dz8,
     a.act8 = act8;
     a.part = part;
     a.G = grad_G(m);
+    constexpr int TW = wg_tile<H>(), SUB = H / TW;  // 128 x 128 tiles per H x H block (hidden > 128)
+    WgJob jobs[MGN_MAX_LAYERS * 3 * SUB * SUB];
     int nj = 0;
     int64_t off = 0;
     for (int l = 0; l < m->n_layers; ++l) {
         int n, k;
         mlp_layer_shape(*m, l, &n, &k);
-        int nkb = cdiv(k, H);
+        int nkb = cdiv(k, H);  // H-wide input blocks (l0_jobs counts these)
         if (l == 0 && l0_jobs > 0 && l0_jobs < nkb) nkb = l0_jobs;
-        for (int kb = 0; kb < nkb; ++kb) {
-            MGN_REQUIRE(nj < 12, "too many weight-gradient jobs");
-            WgJob& j = a.job[nj++];
-            j.layer = l;
-            j.kb = kb;
-            j.n = n;
-            j.k = k;
-            j.kp = act_cols(*m, l);
-            j.staged = gin != nullptr && l == 0;
-            j.zl = l;
-            j.w_off = off;
-            j.b_off = kb == 0 ? off + (int64_t)n * k : -1;
-            j.act_off = act_off(*m, M, l, gin != nullptr);
-        }
+        const int ntb = cdiv(nkb * H < k ? nkb * H : k, TW), nnb = cdiv(n, TW);
+        for (int kb = 0; kb < ntb; ++kb)
+            for (int nb = 0; nb < nnb; ++nb) {
+                MGN_REQUIRE(nj < (int)(sizeof(jobs) / sizeof(jobs[0])), "too many weight-gradient jobs");
+                WgJob& j = jobs[nj++];
+                memset(&j, 0, sizeof(j));
+                j.layer = l;
+                j.kb = kb;
+                j.nb = nb;
+                j.n = n;
+                j.k = k;
+                j.kp = act_cols(*m, l);
+                j.staged = gin != nullptr && l == 0;
+                j.zl = l;
+                j.w_off = off;
+                j.b_off = kb == 0 ? off + (int64_t)n * k : -1;
+                j.act_off = act_off(*m, M, l, gin != nullptr);
+            }
         off += (int64_t)n * k + n;
     }
     a.rows_per_chunk = wgrad_rows_per_chunk(a.RP, nj, H);
     const int nchunks = (int)cdiv64(a.RP, a.rows_per_chunk);
     if (nchunks_out) *nchunks_out = nchunks;
-    if (int e = launch_wgrad_kernel<T, H>(a, nj, nchunks, st)) return e;
+    if (int e = launch_wgrad_kernel<T, H>(a, jobs, nj, nchunks, st)) return e;
     return reduce ? launch_reduce(m, part, nchunks, dscale_part, ntiles, grads, st) : 0;
 }
 
@@ -3438,21 +3474,28 @@ int launch_wgrad_proj(const mgn_mlp* m, int64_t N, const void* dP8, const void* 
     a.dz8 = dP8;
     a.part = part;
     a.G = grad_G(m);
-    for (int s2 = 0; s2 < 2; ++s2) {
-        WgJob& j = a.job[s2];
-        j.layer = 0;
-        j.kb = 1 + s2;
-        j.n = H;
-        j.k = m->in_dim;
-        j.kp = m->in_dim;
-        j.staged = 1;
-        j.zl = s2;
-        j.w_off = 0;
-        j.b_off = -1;
-    }
+    constexpr int TW = wg_tile<H>(), SUB = H / TW;
+    WgJob jobs[2 * SUB * SUB];
+    int nj = 0;
+    for (int s2 = 0; s2 < 2; ++s2)
+        for (int kt = 0; kt < SUB; ++kt)
+            for (int nb = 0; nb < SUB; ++nb) {
+                WgJob& j = jobs[nj++];
+                memset(&j, 0, sizeof(j));
+                j.layer = 0;
+                j.kb = (1 + s2) * SUB + kt;  // W0 columns [(1 + s2) H + kt TW, + TW)
+                j.nb = nb;
+                j.n = H;
+                j.k = m->in_dim;
+                j.kp = m->in_dim;
+                j.staged = 1;
+                j.zl = s2;
+                j.w_off = 0;
+                j.b_off = -1;
+            }
     if (nchunks <= 0) return 0;
     a.rows_per_chunk = (int)(cdiv64(cdiv64(a.RP, nchunks), 64) * 64);
-    return launch_wgrad_kernel<T, H>(a, 2, nchunks, st);
+    return launch_wgrad_kernel<T, H>(a, jobs, nj, nchunks, st);
 }
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -3766,6 +3809,7 @@ size_t mlp_bwd_ws(const mgn_mlp* m, int64_t M) {
         case 32: { constexpr int HH = 32; __VA_ARGS__; } break;                          \
         case 64: { constexpr int HH = 64; __VA_ARGS__; } break;                          \
         case 128: { constexpr int HH = 128; __VA_ARGS__; } break;                        \
+        case 256: { constexpr int HH = 256; __VA_ARGS__; } break;                        \
         default: MGN_REQUIRE(false, "unsupported hidden size");                          \
     }
 

@@ -206,14 +206,14 @@ def forget_topology(edge_index):
 
 
 # --------------------------------------------------------------------------- MLPs and plans
-KERNEL_WIDTHS = (16, 32, 64, 128)
+KERNEL_WIDTHS = (16, 32, 64, 128, 256)
 
 
 def kernel_width(h):
     """The hidden width libmgn's kernels run a model of hidden size h on: h itself when the kernels
     are instantiated for it, else the next such width with zero-padded channels (exact: padded
     weights, biases and RMSNorm scales are 0, so every padded channel stays 0 forward and backward,
-    and the RMSNorm divides by the true h — mgn_mlp.norm_dim). Above 128: unsupported."""
+    and the RMSNorm divides by the true h — mgn_mlp.norm_dim). Above 256: unsupported."""
     for w in KERNEL_WIDTHS:
         if h <= w:
             return w

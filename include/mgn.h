@@ -110,7 +110,7 @@ int mgn_topology_build_async(const int64_t* edge_index, int64_t num_edges, int64
 typedef struct mgn_mlp {
     int32_t n_layers; /* number of nn.Linear (reference nb_of_layers, >= 2)                    */
     int32_t in_dim;   /* input features of Linear 0                                          */
-    int32_t hidden;   /* hidden width the kernels run (16, 32, 64 or 128)                     */
+    int32_t hidden;   /* hidden width the kernels run (16, 32, 64, 128 or 256)                */
     int32_t out_dim;  /* output features of the last Linear (== hidden, or 1..16)            */
     int32_t has_norm; /* RMSNorm(out_dim) after the last Linear                              */
     int32_t dtype;    /* MGN_F32 | MGN_BF16                                                  */
@@ -251,8 +251,8 @@ int mgn_block_backward(const mgn_topology* t, const mgn_mlp* edge, const mgn_mlp
  * until the reduction) and reduce2[0..1] describe the reduction; mgn_wgrad_reduce_many then runs
  * every block's in ONE launch — the same sums in the same order, one launch instead of one per
  * block. Deferred for the chained bf16 h=128 MLPs, the fp32 h=128 ones (fp32 ring) and (ABI v12) the
- * generic hidden 16/32/64 MLPs (one multi-job weight-gradient launch per block); other shapes are
- * reduced at once (reduce2 zeroed: nothing to do). */
+ * generic hidden 16/32/64 MLPs (one multi-job weight-gradient launch per block); other shapes (e.g.
+ * hidden 256: generic kernels, 128 x 128 weight-gradient tiles) are reduced at once (reduce2 zeroed). */
 typedef struct mgn_wgrad_reduce {
     const float* part;
     const float* dsp;

@@ -151,11 +151,15 @@ def _cyl_graph():
 
 @pytest.mark.parametrize("dtype,tf,tg,h", [(torch.float32, 1e-5, None, 128), (torch.bfloat16, 1e-2, 1.5e-1, 128),
                                             (torch.float32, 1e-5, None, 96), (torch.bfloat16, 1e-2, 1.5e-1, 96),
-                                            (torch.float32, 1e-5, None, 24), (torch.float32, 1e-5, None, 36)])
+                                            (torch.float32, 1e-5, None, 24), (torch.float32, 1e-5, None, 36),
+                                            (torch.float32, 1e-5, None, 192), (torch.bfloat16, 1e-2, 1.5e-1, 192),
+                                            (torch.float32, 1e-5, None, 256), (torch.bfloat16, 1e-2, 1.5e-1, 256)])
 def test_block_cylinder_h128_vs_oracle(dtype, tf, tg, h):
     """One GraphNetBlock on the CylinderFlow mesh vs the oracle. h = 96, 36 and 24 are not kernel
     widths: they run zero-padded to 128 / 64 / 32 (_engine.kernel_width; exact — same bounds as
-    h = 128). Sizes chosen without a ReLU tie on this input (no pre-activation within 1e-6 of its
+    h = 128). Hidden sizes above 128: h = 256 on the 256-wide generic kernels
+    (weight gradients in 128 x 128 tiles), h = 192 zero-padded to 256 — at the h = 128 bounds.
+    Sizes chosen without a ReLU tie on this input (no pre-activation within 1e-6 of its
     layer's mean |z| in fp64; h = 40 has one at 8e-8, where any fp32 order may flip the unit)."""
     from graphphysics.models.layers import GraphNetBlock
 
@@ -268,11 +272,12 @@ def test_epd_cylinder_vs_oracle(mp, h, dtype, tf, tg):
 
 
 @pytest.mark.parametrize("h,dtype", [(36, torch.float32), (48, torch.float32), (48, torch.bfloat16),
-                                     (64, torch.bfloat16), (100, torch.float32), (100, torch.bfloat16)])
+                                     (64, torch.bfloat16), (100, torch.float32), (100, torch.bfloat16),
+                                     (192, torch.float32), (192, torch.bfloat16)])
 def test_epd_any_hidden_size_vs_oracle(h, dtype):
     """EncodeProcessDecode with hidden sizes the kernels are not instantiated for (the reference's
     build_mlp takes any size: layers.py:77-113): zero-padded to the next kernel width (48 -> 64 on
-    the generic kernels, 100 -> 128 on the chained bf16 ones), with the RMSNorm over the true h.
+    the generic kernels, 100 -> 128 on the chained bf16 ones, 192 -> 256), with the RMSNorm over the true h.
     Bounds as test_epd_cylinder_vs_oracle: fp32 output 1e-4 and gradients vs fp64 no worse than the
     reference fp32 path; bf16 no further from fp64 than 2 x PyTorch's bf16 autocast (whole
     gradient; 4 x per parameter). h = 64 (bf16) is the unpadded control on the same generic kernels
@@ -676,6 +681,26 @@ def test_training_matches_golden_losses_fp32():
         sch.step()
         losses.append(loss.item())
     np.testing.assert_allclose(losses, z["cfgA/losses"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_captured_training_step_hidden_192(dtype):
+    """Training at a hidden size above 128: h = 192 runs zero-padded on the
+    256-wide kernels; the captured TrainStep (hipGraph, concurrent weight-gradient stream) takes the
+    same 3 steps as the eager one, and the loss falls."""
+    from graphphysics.training.step import TrainStep
+
+    res = []
+    for graph in (False, True):
+        sim, opt, sch, data = _cyl_train_setup(dtype, mp=2, h=192, batch=1)
+        st = TrainStep(sim, opt, sch, data, graph=graph)
+        losses = [float(st().item()) for _ in range(3)]
+        torch.cuda.synchronize()
+        res.append((losses, [p.detach().clone() for p in sim.parameters()]))
+    assert all(np.isfinite(res[0][0])) and res[0][0][-1] < res[0][0][0], res[0][0]
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6)
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.parametrize("conc", ["auto", "0,0", "160,96"])

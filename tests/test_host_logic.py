@@ -223,7 +223,7 @@ def test_load_checkpoint_updates_normalizer_buffers_in_place(tmp_path):
         assert torch.equal(nb._acc_sum, na._acc_sum) and float(nb._acc_count) == 7.0
 
 
-@pytest.mark.parametrize("h", [48, 96, 100, 128])
+@pytest.mark.parametrize("h", [48, 96, 100, 128, 192, 256])
 def test_padded_plan_layout_round_trips(h):
     """Hidden sizes the kernels are not instantiated for run zero-padded to the next kernel width
     (_engine.kernel_width): the padded parameter layout the kernels write gradients in must map
@@ -255,8 +255,9 @@ def test_padded_plan_layout_round_trips(h):
     assert dec.shapes[0][:2] == (W, W) and dec.shapes[0][4:] == (h, W)
     enc = plan.specs[0]  # the node encoder reads the raw 11 features: not padded
     assert enc.shapes[0][:2] == (W, 11) and enc.out_width == W
-    with pytest.raises(ValueError, match="at most 128"):
-        _engine.kernel_width(144)
+    assert _engine.kernel_width(144) == 256  # hidden > 128: the 256-wide kernels (128 x 128 weight-gradient tiles)
+    with pytest.raises(ValueError, match="at most 256"):
+        _engine.kernel_width(257)
 
 
 def test_data_parallel_step_refuses_to_continue_after_validation_error():
