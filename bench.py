@@ -42,8 +42,10 @@ HBM_PEAK = 8000.0  # GB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 100 timed steps (0.3 s at Cfg B) after 20 warm-up replays: a 20-step window carried ~1.6 % of fixed
+    # start-up cost (same box: 343.9 -> 349.6 steps/s, tools/dev/r06_steps.sh)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=8, help="graphs per GPU")
     ap.add_argument("--mp", type=int, default=15)
     ap.add_argument("--hidden", type=int, default=128)
