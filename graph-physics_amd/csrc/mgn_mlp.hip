@@ -2191,7 +2191,6 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
     float* act = reinterpret_cast<float*>(a.act8);
     const int64_t r8 = f32c_r8t(row, g);  // transposed R8 saves
     const float* res = reinterpret_cast<const float*>(a.resid);
-    f4 rv[8];
     const int wave = threadIdx.x >> 6;
     const float* pk2 = pk;  // MGN_F32C_FLOW: layer l's chain image at pk2 + (l - 1) * step + image offset
     const int64_t pstep = linear_pack_elems(H, H, MGN_F32);
@@ -2208,13 +2207,6 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
             nxt = pk + chain_image_off(H, H);
             if (F32C_NBUF == 2) f32c_stage(nxt, (l & 1) ? img0 : img1);
             pk += linear_pack_elems(H, H, MGN_F32);
-        }
-        if (l == 3) {
-            // the residual lands during the last GEMM
-#pragma unroll
-            for (int nt = 0; nt < 8; ++nt)
-                rv[nt] = (res && valid) ? *reinterpret_cast<const f4*>(res + row * H + 16 * nt + 4 * g)
-                                        : f4{0.f, 0.f, 0.f, 0.f};
         }
         // layer l's input (the ReLU output of layer l-1) is saved while it feeds the MFMAs
         // (save pointers by selection: a kernel-argument array indexed at run time is copied to scratch)
@@ -2270,6 +2262,13 @@ __global__ F32C_BOUNDS void edge_fwd_f32_chain_kernel(FwdArgs a) {
             F32C_STAMP(3);
         }
     }
+    // the residual rows after the last GEMM (round 6: loaded during it, their 32 registers on top of the
+    // GEMM's made the kernel spill ~33 registers per lane at the 168-register cap; now 138, no spills:
+    // edge forward 153 -> 144 us at fp32 Cfg B, profiles/r06_fp32_ab.txt)
+    f4 rv[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+        rv[nt] = (res && valid) ? *reinterpret_cast<const f4*>(res + row * H + 16 * nt + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
     // last Linear (bias in the accumulator): RMSNorm over the row's 128 features (4 lanes of 32), residual
     float ss = 0.f;
 #pragma unroll
