@@ -2713,6 +2713,250 @@ __global__ F32N_BOUNDS void node_fwd_f32_chain_kernel(FwdArgs a) {
     F32C_STAMP_PRINT("f32nf");
 }
 
+// Split form (round 6, MGN_F32N_SPLIT): the same node MLP with TWO waves per 16-row tile — wave 2p + h owns
+// output features 64h .. 64h + 63 (n-tiles 4h .. 4h + 3) of every layer — so a workgroup runs 8 waves
+// (two per SIMD) on the same 64 rows, and one wave's aggregation gathers, LDS waits and barrier slack
+// overlap the other's MFMAs (the one-wave-per-SIMD form above ran its MFMA pipe 31 % busy). The halves
+// meet in LDS: each layer's ReLU output (the next layer's B operand) and the last layer's accumulators
+// are exchanged between the two waves of a tile. Per accumulator the same MFMAs in the same k order, the
+// aggregate's terms per feature in the same edge order, the RMSNorm sum in the same order: the results
+// are bit-identical to the one-wave form. LDS: the two 64 KiB images + 4 KiB of exchange per wave (the
+// biases and scales come from L2, a layer ahead).
+#ifndef MGN_F32N_SPLIT
+#define MGN_F32N_SPLIT 1
+#endif
+constexpr int F32S_WAVES = 8;
+#define F32S_BOUNDS __launch_bounds__(F32S_WAVES * 64, 2)
+constexpr size_t F32S_LDS_FWD = 2 * F32C_LAYER * sizeof(float) + (size_t)F32S_WAVES * 4 * 64 * sizeof(f4);
+static_assert(F32S_LDS_FWD <= 160 * 1024, "split fp32 node forward: LDS");
+
+__device__ __forceinline__ void f32s_stage(const float* __restrict__ src, float* img) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int c = wave; c < F32C_LAYER / 256; c += F32S_WAVES) glds16(src + c * 256 + lane * 4, img + c * 256);
+}
+
+// acc[j] += n-tile 4nh + j of X·Wᵀ (all 32 k-steps, f32c_gemm's k order); save: the k-groups t of this
+// wave's half of the input's R8 save (the partner stores the other half)
+template <int nh>
+__device__ __forceinline__ void f32s_gemm(f4 (&acc)[4], const f4 (&x)[8], const float* img, int lane,
+                                          float* save = nullptr) {
+    f4 w[2][4];
+    const f4* ip = reinterpret_cast<const f4*>(img) + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[0][j] = ip[((4 * nh + j) * 8 + 0) * 64];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        if (t + 1 < 8) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[(t + 1) & 1][j] = ip[((4 * nh + j) * 8 + t + 1) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[t & 1][j][r], x[t][r], acc[j], 0, 0, 0);
+        if (save && (t >> 2) == nh) *reinterpret_cast<f4*>(save + 128 * t) = quad_transpose(x[t], lane);
+    }
+}
+
+// the half is a template parameter: register arrays indexed by it stay statically indexed (a run-time
+// half made the compiler move them with indexed register moves: 4x slower)
+template <int nh>
+__device__ __forceinline__ void node_fwd_f32_split_body(const FwdArgs& a) {
+    constexpr int H = 128;
+    constexpr int AG = MGN_F32N_AG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* const img0 = reinterpret_cast<float*>(smem);
+    float* const img1 = img0 + F32C_LAYER;
+    f4* const xch = reinterpret_cast<f4*>(img1 + F32C_LAYER);  // [wave][4][64]
+    const int lane = threadIdx.x & 63, g = lane >> 4, ri = lane & 15, wave = threadIdx.x >> 6;
+    f4* const mine = xch + (size_t)wave * 256 + lane;
+    const f4* const theirs = xch + (size_t)(wave ^ 1) * 256 + lane;
+    const int64_t tile = (int64_t)blockIdx.x * (F32S_WAVES / 2) + (wave >> 1);
+    const int64_t row = tile * 16 + ri;
+    const bool valid = row < a.M;
+    const float* pk = reinterpret_cast<const float*>(a.wpack);
+    f32s_stage(pk + chain_image_off(H, 2 * H, 0), img0);
+    f32s_stage(pk + chain_image_off(H, 2 * H, 1), img1);
+    pk += linear_pack_elems(H, 2 * H, MGN_F32);
+    // layer 0's bias half, then each next layer's one layer ahead
+    f4 bias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias[j] = ld4u(a.bias[0] + 16 * (4 * nh + j) + 4 * g);
+    // phase A: x rows (whole: layer 0's x-block operand and the residual), this wave's half of the aggregate
+    const int64_t rowc = valid ? row : a.M - 1;
+    const float* x = reinterpret_cast<const float*>(a.seg[0].p);
+    f4 xr[8], ag[8], sc[4];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) xr[t] = *reinterpret_cast<const f4*>(x + rowc * a.seg[0].ld + 16 * t + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        sc[j] = ld4u(a.agg_scale + 16 * (4 * nh + j) + 4 * g);
+        ag[4 * nh + j] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    {
+        const int kb = a.seg_ptr[rowc], ke = valid ? a.seg_ptr[rowc + 1] : kb;
+        const float* z = reinterpret_cast<const float*>(a.agg_z);
+#pragma unroll 1
+        for (int k = kb; k < ke; k += AG) {
+            f4 zz[AG][4];
+            float qq[AG];
+#pragma unroll
+            for (int u = 0; u < AG; ++u) {
+                const int64_t ku = k + u < ke ? k + u : ke - 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) zz[u][j] = *reinterpret_cast<const f4*>(z + ku * H + 16 * (4 * nh + j) + 4 * g);
+                qq[u] = a.agg_rden[ku];
+            }
+#pragma unroll
+            for (int u = 0; u < AG; ++u) {
+                if (k + u >= ke) break;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) ag[4 * nh + j][r] += sc[j][r] * (zz[u][j][r] / qq[u]);
+            }
+        }
+    }
+    if (!valid) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) xr[t] = f4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            st4(reinterpret_cast<float*>(a.agg_save) + row * H + 16 * (4 * nh + j) + 4 * g, ag[4 * nh + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mine[64 * j] = ag[4 * nh + j];
+    f32c_stage_wait();
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ag[4 * (1 - nh) + j] = theirs[64 * j];
+    f4 acc[4], x1[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bias[j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias[j] = ld4u(a.bias[1] + 16 * (4 * nh + j) + 4 * g);
+    f32s_gemm<nh>(acc, xr, img0, lane);  // x block
+    __syncthreads();                     // every wave is done with img0 (and has read its partner's aggregate)
+    f32s_stage(pk + chain_image_off(H, H), img0);
+    pk += linear_pack_elems(H, H, MGN_F32);
+    f32s_gemm<nh>(acc, ag, img1, lane);  // aggr block
+    float* act = reinterpret_cast<float*>(a.act8);
+    const int64_t r8 = f32c_r8t(row, g);
+    // ReLU of this wave's half -> the exchange; ballot words nt*4 + r (nt = 4nh + j) from lane nt*4 + r
+    auto relu_half = [&](int l) {
+        unsigned long long word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = fmaxf(acc[j][r], 0.f);
+                x1[4 * nh + j][r] = v;
+                const unsigned long long bits = __ballot(v > 0.f);
+                if (lane == (4 * nh + j) * 4 + r) word = bits;
+            }
+            mine[64 * j] = x1[4 * nh + j];
+        }
+        if ((lane >> 4) == nh && lane < 32) a.mask[(int64_t)l * a.mask_stride + tile * 32 + lane] = word;
+    };
+    relu_half(0);
+    f32c_stage_wait();
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x1[4 * (1 - nh) + j] = theirs[64 * j];
+    __syncthreads();  // the partner's half is read before either wave writes the exchange again
+#pragma unroll 1
+    for (int l = 1; l < 4; ++l) {
+        float* cur = (l & 1) ? img0 : img1;
+        if (l < 3) {
+            f32s_stage(pk + chain_image_off(H, H), (l & 1) ? img1 : img0);
+            pk += linear_pack_elems(H, H, MGN_F32);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = bias[j];
+        const float* bn = l == 1 ? a.bias[2] : a.bias[3];
+        if (l < 3) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bias[j] = ld4u(bn + 16 * (4 * nh + j) + 4 * g);
+        }
+        float* sv = l == 1 ? act + a.act_off[1] : l == 2 ? act + a.act_off[2] : act + a.act_off[3];
+        if (l == 3 && a.pn_pack) f32s_stage(a.pn_pack + chain_image_off(H, 3 * H, 1), img1);
+        f32s_gemm<nh>(acc, x1, cur, lane, sv + r8);
+        if (l < 3) {
+            relu_half(l);
+            f32c_stage_wait();
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x1[4 * (1 - nh) + j] = theirs[64 * j];
+            __syncthreads();
+        }
+    }
+    // last Linear: the two halves of the accumulators meet, RMSNorm in the one-wave form's order
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mine[64 * j] = acc[j];
+    __syncthreads();
+    f4 full[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        full[4 * nh + j] = acc[j];
+        full[4 * (1 - nh) + j] = theirs[64 * j];
+    }
+    float ss = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss += full[nt][r] * full[nt][r];
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    {
+        const float q = sqrtf(ss) * a.dinv + RMS_EPS;
+        if (valid && g == 0 && nh == 0) a.rden_save[row] = q;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {
+            const int n = 16 * nt + 4 * g;
+            const f4 s = ld4u(a.scale + n);
+            f4 y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = s[r] * (full[nt][r] / q);
+            y = xr[nt] + y;
+            if (valid && (nt >> 2) == nh) {
+                st4(reinterpret_cast<float*>(a.z_save) + row * H + n, full[nt]);
+                st4(reinterpret_cast<float*>(a.out) + row * a.out_ld + n, y);
+            }
+            x1[nt] = valid ? y : f4{0.f, 0.f, 0.f, 0.f};  // x_out: the projections' B operand
+        }
+    }
+    if (!a.pn_pack) return;
+    // the NEXT block's node projections from x_out, this wave's half of each ([x·W0bᵀ ‖ x·W0cᵀ])
+    f32c_stage_wait();
+    __syncthreads();  // W0b landed; every wave is done with img0 (layer 3)
+    f32s_stage(a.pn_pack + chain_image_off(H, 3 * H, 2), img0);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+        f32s_gemm<nh>(acc, x1, half ? img0 : img1, lane);
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                st4(a.pn_out + row * (2 * H) + half * H + 16 * (4 * nh + j) + 4 * g, acc[j]);
+        }
+        if (half == 0) {
+            f32c_stage_wait();
+            __syncthreads();
+        }
+    }
+}
+
+__global__ F32S_BOUNDS void node_fwd_f32_split_kernel(FwdArgs a) {
+    if ((threadIdx.x >> 6) & 1)  // wave-uniform: both bodies pass the same barriers
+        node_fwd_f32_split_body<1>(a);
+    else
+        node_fwd_f32_split_body<0>(a);
+}
+
 __global__ F32N_BOUNDS void node_bwd_f32_chain_kernel(BwdArgs a) {
     constexpr int H = 128;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2991,12 +3235,19 @@ int launch_fwd(const mgn_mlp* m, const MlpIn& in, int64_t M, void* out, int out_
             al16(a.out) && !a.ablate) {
             const int grid = (int)(rows_pad(M) / (16 * F32N_WAVES));
             if (grid == 0) return 0;
-            if (int e = set_lds((const void*)node_fwd_f32_chain_kernel, F32N_LDS_FWD)) return e;
             if (in.pn_pack && in.pn_out) {
                 a.pn_pack = in.pn_pack;
                 a.pn_out = in.pn_out;
                 if (in.pn_done) *in.pn_done = 1;
             }
+            if (MGN_F32N_SPLIT) {
+                if (int e = set_lds((const void*)node_fwd_f32_split_kernel, F32S_LDS_FWD)) return e;
+                ProfScope ps(PROF_FWD_NODE, st);
+                hipLaunchKernelGGL(node_fwd_f32_split_kernel, dim3(grid), dim3(F32S_WAVES * 64), F32S_LDS_FWD, st, a);
+                MGN_LAUNCH_CHECK();
+                return 0;
+            }
+            if (int e = set_lds((const void*)node_fwd_f32_chain_kernel, F32N_LDS_FWD)) return e;
             ProfScope ps(PROF_FWD_NODE, st);
             hipLaunchKernelGGL(node_fwd_f32_chain_kernel, dim3(grid), dim3(F32N_WAVES * 64), F32N_LDS_FWD, st, a);
             MGN_LAUNCH_CHECK();
