@@ -44,7 +44,8 @@ def kernel_class(name):
                      ("chain16_dense_fwd_kernel", "fwd_dense"), ("chain16_dense_bwd_kernel", "bwd_dense"),
                      ("chain16_fwd_kernel", "fwd_edge"), ("chain16_bwd_kernel", "bwd_edge"),
                      ("edge_fwd_f32_chain_kernel", "fwd_edge"), ("edge_bwd_f32_chain_kernel", "bwd_edge"),
-                     ("node_fwd_f32_chain_kernel", "fwd_node"), ("node_bwd_f32_chain_kernel", "bwd_node"),
+                     ("node_fwd_f32_chain_kernel", "fwd_node"), ("node_fwd_f32_split_kernel", "fwd_node"),
+                     ("node_bwd_f32_chain_kernel", "bwd_node"),
                      ("mlp_wgrad_kernel", "wgrad_dense"), ("wgrad_ring_kernel", "wgrad"),
                      ("wgrad_ring_f32_kernel", "wgrad"), ("chain16_rew_kernel", "wgrad"),
                      ("wgrad_reduce_kernel", "wgrad_reduce"), ("node_grad_kernel", "combine"),
